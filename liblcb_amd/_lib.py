@@ -1,0 +1,87 @@
+"""ctypes binding of the in-tree C-ABI library liblcb_hash_gpu.so.
+
+The library is the product: every digest computed through this package is
+computed by its HIP kernels.  If the library is missing, or no MI355X is
+visible, calls raise instead of falling back to anything on the CPU.
+
+torch is imported first on purpose: torch ships its own libamdhip64 (soname
+libamdhip64.so.7); loading it before our library makes both share ONE HIP
+runtime, so torch tensors, streams and events interoperate with our kernels.
+"""
+import ctypes
+import errno
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblcb_hash_gpu.so")
+
+MD5, SHA1, SHA224, SHA256, SHA384, SHA512, GOST256, GOST512 = range(1, 9)
+ALG_NAMES = {MD5: "md5", SHA1: "sha1", SHA224: "sha224", SHA256: "sha256",
+             SHA384: "sha384", SHA512: "sha512", GOST256: "gost256", GOST512: "gost512"}
+ALG_IDS = {v: k for k, v in ALG_NAMES.items()}
+DIGEST_SIZE = {MD5: 16, SHA1: 20, SHA224: 28, SHA256: 32, SHA384: 48, SHA512: 64,
+               GOST256: 32, GOST512: 64}
+BLOCK_SIZE = {a: (128 if a in (SHA384, SHA512) else 64) for a in DIGEST_SIZE}
+F_DEVICE = 0x1
+
+_lib = None
+
+c_sz = ctypes.c_size_t
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) for every symbol include/lcb_hash_gpu.h declares.
+_PLAIN = [c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32, c_vp]
+_HMAC = [c_vp, c_sz] + _PLAIN
+SIGNATURES = [
+    ("lcb_hash_gpu_abi_version", ctypes.c_int, []),
+    ("lcb_hash_digest_size", c_sz, [ctypes.c_int]),
+    ("lcb_hash_block_size", c_sz, [ctypes.c_int]),
+    ("lcb_hash_gpu_device_count", ctypes.c_int, []),
+    ("lcb_hash_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("lcb_hash_batch", ctypes.c_int, [ctypes.c_int, c_vp, c_sz] + _PLAIN),
+    ("md5_get_digest_batch", ctypes.c_int, _PLAIN),
+    ("md5_hmac_get_digest_batch", ctypes.c_int, _HMAC),
+    ("sha1_get_digest_batch", ctypes.c_int, _PLAIN),
+    ("sha1_hmac_get_digest_batch", ctypes.c_int, _HMAC),
+    ("sha2_get_digest_batch", ctypes.c_int,
+     [c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("sha2_hmac_get_digest_batch", ctypes.c_int,
+     [c_sz, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("gost3411_2012_get_digest_batch", ctypes.c_int,
+     [c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("gost3411_2012_hmac_get_digest_batch", ctypes.c_int,
+     [c_sz, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("lcb_hash_gen_synthetic", ctypes.c_int, [c_u64, c_u64, c_vp, c_sz, c_vp]),
+    ("lcb_hash_gpu_gost_table", ctypes.c_int, [c_vp]),
+]
+
+
+class LcbHashError(OSError):
+    """A non-zero liblcb-style errno from the C-ABI."""
+
+
+def lib():
+    """The loaded library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("%s is missing: build it with `python -c 'import __graft_entry__ as g; "
+                               "g.build()'` (or `make -C liblcb_amd`)" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().lcb_hash_strerror(rc).decode()
+        raise LcbHashError(rc, "liblcb_hash_gpu: %s (%s)" % (msg, errno.errorcode.get(rc, rc)))
+    return rc

@@ -1,0 +1,250 @@
+// gost_device.hpp — GOST R 34.11-2012 (Streebog, RFC 6986) per-lane device
+// code for the MI355X batch kernels.
+//
+// One lane per message (as the MD family).  The LPS transform uses the
+// big-table form of the reference (gost3411-2012.h:1071-1099):
+//     dst[i] = XOR_{j=0..7} Ax[j][ byte i of src[j] ]
+// with the 8 x 256 x u64 = 16 KiB table held in LDS (one copy per workgroup),
+// so LPS is 64 ds_read_b64 + 56 XORs per 512-bit transform and a 64-byte
+// block costs 25 LPS (gost3411-2012.h:1129-1142).  The table is generated at
+// COMPILE TIME from the RFC 6986 S-box pi and the 64 rows of the linear map A,
+// following the reference's small-table definition (gost3411-2012.h:1032-1067),
+// and pinned against the reference's gost3411_2012_Ax by a test.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "hash_device.hpp"
+
+namespace lcbgpu {
+
+struct GostConsts {
+    uint8_t pi[256];
+    uint64_t A[64];
+    uint64_t C[12][8];
+};
+
+// RFC 6986 section 6: pi, A, C.
+constexpr GostConsts kGostConsts = {
+    {0xfc, 0xee, 0xdd, 0x11, 0xcf, 0x6e, 0x31, 0x16, 0xfb, 0xc4, 0xfa, 0xda, 0x23, 0xc5, 0x04, 0x4d,
+     0xe9, 0x77, 0xf0, 0xdb, 0x93, 0x2e, 0x99, 0xba, 0x17, 0x36, 0xf1, 0xbb, 0x14, 0xcd, 0x5f, 0xc1,
+     0xf9, 0x18, 0x65, 0x5a, 0xe2, 0x5c, 0xef, 0x21, 0x81, 0x1c, 0x3c, 0x42, 0x8b, 0x01, 0x8e, 0x4f,
+     0x05, 0x84, 0x02, 0xae, 0xe3, 0x6a, 0x8f, 0xa0, 0x06, 0x0b, 0xed, 0x98, 0x7f, 0xd4, 0xd3, 0x1f,
+     0xeb, 0x34, 0x2c, 0x51, 0xea, 0xc8, 0x48, 0xab, 0xf2, 0x2a, 0x68, 0xa2, 0xfd, 0x3a, 0xce, 0xcc,
+     0xb5, 0x70, 0x0e, 0x56, 0x08, 0x0c, 0x76, 0x12, 0xbf, 0x72, 0x13, 0x47, 0x9c, 0xb7, 0x5d, 0x87,
+     0x15, 0xa1, 0x96, 0x29, 0x10, 0x7b, 0x9a, 0xc7, 0xf3, 0x91, 0x78, 0x6f, 0x9d, 0x9e, 0xb2, 0xb1,
+     0x32, 0x75, 0x19, 0x3d, 0xff, 0x35, 0x8a, 0x7e, 0x6d, 0x54, 0xc6, 0x80, 0xc3, 0xbd, 0x0d, 0x57,
+     0xdf, 0xf5, 0x24, 0xa9, 0x3e, 0xa8, 0x43, 0xc9, 0xd7, 0x79, 0xd6, 0xf6, 0x7c, 0x22, 0xb9, 0x03,
+     0xe0, 0x0f, 0xec, 0xde, 0x7a, 0x94, 0xb0, 0xbc, 0xdc, 0xe8, 0x28, 0x50, 0x4e, 0x33, 0x0a, 0x4a,
+     0xa7, 0x97, 0x60, 0x73, 0x1e, 0x00, 0x62, 0x44, 0x1a, 0xb8, 0x38, 0x82, 0x64, 0x9f, 0x26, 0x41,
+     0xad, 0x45, 0x46, 0x92, 0x27, 0x5e, 0x55, 0x2f, 0x8c, 0xa3, 0xa5, 0x7d, 0x69, 0xd5, 0x95, 0x3b,
+     0x07, 0x58, 0xb3, 0x40, 0x86, 0xac, 0x1d, 0xf7, 0x30, 0x37, 0x6b, 0xe4, 0x88, 0xd9, 0xe7, 0x89,
+     0xe1, 0x1b, 0x83, 0x49, 0x4c, 0x3f, 0xf8, 0xfe, 0x8d, 0x53, 0xaa, 0x90, 0xca, 0xd8, 0x85, 0x61,
+     0x20, 0x71, 0x67, 0xa4, 0x2d, 0x2b, 0x09, 0x5b, 0xcb, 0x9b, 0x25, 0xd0, 0xbe, 0xe5, 0x6c, 0x52,
+     0x59, 0xa6, 0x74, 0xd2, 0xe6, 0xf4, 0xb4, 0xc0, 0xd1, 0x66, 0xaf, 0xc2, 0x39, 0x4b, 0x63, 0xb6},
+    {0x8e20faa72ba0b470ull, 0x47107ddd9b505a38ull, 0xad08b0e0c3282d1cull, 0xd8045870ef14980eull,
+     0x6c022c38f90a4c07ull, 0x3601161cf205268dull, 0x1b8e0b0e798c13c8ull, 0x83478b07b2468764ull,
+     0xa011d380818e8f40ull, 0x5086e740ce47c920ull, 0x2843fd2067adea10ull, 0x14aff010bdd87508ull,
+     0x0ad97808d06cb404ull, 0x05e23c0468365a02ull, 0x8c711e02341b2d01ull, 0x46b60f011a83988eull,
+     0x90dab52a387ae76full, 0x486dd4151c3dfdb9ull, 0x24b86a840e90f0d2ull, 0x125c354207487869ull,
+     0x092e94218d243cbaull, 0x8a174a9ec8121e5dull, 0x4585254f64090fa0ull, 0xaccc9ca9328a8950ull,
+     0x9d4df05d5f661451ull, 0xc0a878a0a1330aa6ull, 0x60543c50de970553ull, 0x302a1e286fc58ca7ull,
+     0x18150f14b9ec46ddull, 0x0c84890ad27623e0ull, 0x0642ca05693b9f70ull, 0x0321658cba93c138ull,
+     0x86275df09ce8aaa8ull, 0x439da0784e745554ull, 0xafc0503c273aa42aull, 0xd960281e9d1d5215ull,
+     0xe230140fc0802984ull, 0x71180a8960409a42ull, 0xb60c05ca30204d21ull, 0x5b068c651810a89eull,
+     0x456c34887a3805b9ull, 0xac361a443d1c8cd2ull, 0x561b0d22900e4669ull, 0x2b838811480723baull,
+     0x9bcf4486248d9f5dull, 0xc3e9224312c8c1a0ull, 0xeffa11af0964ee50ull, 0xf97d86d98a327728ull,
+     0xe4fa2054a80b329cull, 0x727d102a548b194eull, 0x39b008152acb8227ull, 0x9258048415eb419dull,
+     0x492c024284fbaec0ull, 0xaa16012142f35760ull, 0x550b8e9e21f7a530ull, 0xa48b474f9ef5dc18ull,
+     0x70a6a56e2440598eull, 0x3853dc371220a247ull, 0x1ca76e95091051adull, 0x0edd37c48a08a6d8ull,
+     0x07e095624504536cull, 0x8d70c431ac02a736ull, 0xc83862965601dd1bull, 0x641c314b2b8ee083ull},
+    {{0xdd806559f2a64507ull, 0x05767436cc744d23ull, 0xa2422a08a460d315ull, 0x4b7ce09192676901ull,
+      0x714eb88d7585c4fcull, 0x2f6a76432e45d016ull, 0xebcb2f81c0657c1full, 0xb1085bda1ecadae9ull},
+     {0xe679047021b19bb7ull, 0x55dda21bd7cbcd56ull, 0x5cb561c2db0aa7caull, 0x9ab5176b12d69958ull,
+      0x61d55e0f16b50131ull, 0xf3feea720a232b98ull, 0x4fe39d460f70b5d7ull, 0x6fa3b58aa99d2f1aull},
+     {0x991e96f50aba0ab2ull, 0xc2b6f443867adb31ull, 0xc1c93a376062db09ull, 0xd3e20fe490359eb1ull,
+      0xf2ea7514b1297b7bull, 0x06f15e5f529c1f8bull, 0x0a39fc286a3d8435ull, 0xf574dcac2bce2fc7ull},
+     {0x220cbebc84e3d12eull, 0x3453eaa193e837f1ull, 0xd8b71333935203beull, 0xa9d72c82ed03d675ull,
+      0x9d721cad685e353full, 0x488e857e335c3c7dull, 0xf948e1a05d71e4ddull, 0xef1fdfb3e81566d2ull},
+     {0x601758fd7c6cfe57ull, 0x7a56a27ea9ea63f5ull, 0xdfff00b723271a16ull, 0xbfcd1747253af5a3ull,
+      0x359e35d7800fffbdull, 0x7f151c1f1686104aull, 0x9a3f410c6ca92363ull, 0x4bea6bacad474799ull},
+     {0xfa68407a46647d6eull, 0xbf71c57236904f35ull, 0x0af21f66c2bec6b6ull, 0xcffaa6b71c9ab7b4ull,
+      0x187f9ab49af08ec6ull, 0x2d66c4f95142a46cull, 0x6fa4c33b7a3039c0ull, 0xae4faeae1d3ad3d9ull},
+     {0x8886564d3a14d493ull, 0x3517454ca23c4af3ull, 0x06476983284a0504ull, 0x0992abc52d822c37ull,
+      0xd3473e33197a93c9ull, 0x399ec6c7e6bf87c9ull, 0x51ac86febf240954ull, 0xf4c70e16eeaac5ecull},
+     {0xa47f0dd4bf02e71eull, 0x36acc2355951a8d9ull, 0x69d18d2bd1a5c42full, 0xf4892bcb929b0690ull,
+      0x89b4443b4ddbc49aull, 0x4eb7f8719c36de1eull, 0x03e7aa020c6e4141ull, 0x9b1f5b424d93c9a7ull},
+     {0x7261445183235adbull, 0x0e38dc92cb1f2a60ull, 0x7b2b8a9aa6079c54ull, 0x800a440bdbb2ceb1ull,
+      0x3cd955b7e00d0984ull, 0x3a7d3a1b25894224ull, 0x944c9ad8ec165fdeull, 0x378f5a541631229bull},
+     {0x74b4c7fb98459cedull, 0x3698fad1153bb6c3ull, 0x7a1e6c303b7652f4ull, 0x9fe76702af69334bull,
+      0x1fffe18a1b336103ull, 0x8941e71cff8a78dbull, 0x382ae548b2e4f3f3ull, 0xabbedea680056f52ull},
+     {0x6bcaa4cd81f32d1bull, 0xdea2594ac06fd85dull, 0xefbacd1d7d476e98ull, 0x8a1d71efea48b9caull,
+      0x2001802114846679ull, 0xd8fa6bbbebab0761ull, 0x3002c6cd635afe94ull, 0x7bcd9ed0efc889fbull},
+     {0x48bc924af11bd720ull, 0xfaf417d5d9b21b99ull, 0xe71da4aa88e12852ull, 0x5d80ef9d1891cc86ull,
+      0xf82012d430219f9bull, 0xcda43c32bcdf1d77ull, 0xd21380b00449b17aull, 0x378ee767f11631baull}}};
+
+struct GostAx {
+    uint64_t t[8][256];
+};
+
+// Ax[j][b] = L(pi[b] placed in byte j): bit s of byte j is bit 8j+s of the
+// 64-bit row, which selects A[63 - 8j - s] (MSB-first, gost3411-2012.h:1056-1064).
+constexpr GostAx make_gost_ax() {
+    GostAx r{};
+    for (int j = 0; j < 8; ++j)
+        for (int b = 0; b < 256; ++b) {
+            uint64_t c = 0;
+            const unsigned v = kGostConsts.pi[b];
+            for (int s = 0; s < 8; ++s)
+                if ((v >> s) & 1u) c ^= kGostConsts.A[63 - 8 * j - s];
+            r.t[j][b] = c;
+        }
+    return r;
+}
+
+constexpr GostAx kGostAxHost = make_gost_ax();
+__device__ const GostAx kGostAxDev = make_gost_ax();
+__constant__ const uint64_t kGostC[12][8] = {
+#define LCB_C(i) {kGostConsts.C[i][0], kGostConsts.C[i][1], kGostConsts.C[i][2], kGostConsts.C[i][3], \
+                  kGostConsts.C[i][4], kGostConsts.C[i][5], kGostConsts.C[i][6], kGostConsts.C[i][7]}
+    LCB_C(0), LCB_C(1), LCB_C(2), LCB_C(3), LCB_C(4), LCB_C(5),
+    LCB_C(6), LCB_C(7), LCB_C(8), LCB_C(9), LCB_C(10), LCB_C(11)
+#undef LCB_C
+};
+
+// Cooperative copy of the 16 KiB table into LDS (call by every thread, then barrier).
+__device__ __forceinline__ void gost_stage_table(uint64_t* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(&kGostAxDev.t[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+// LPS(x) (gost3411-2012.h:1071-1090).
+__device__ __forceinline__ void gost_lps(uint64_t o[8], const uint64_t x[8], const uint64_t* __restrict__ T) {
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { lo[j] = (uint32_t)x[j]; hi[j] = (uint32_t)(x[j] >> 32); }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t src = (i < 4) ? lo[j] : hi[j];
+            const uint32_t b = __builtin_amdgcn_ubfe(src, 8u * (i & 3), 8u);
+            acc ^= T[j * 256 + b];
+        }
+        o[i] = acc;
+    }
+}
+
+// g_N(h, m) for a counter N whose upper 448 bits are zero (messages shorter
+// than 2^61 bytes; the ABI caps lengths at 2^32): gost3411-2012.h:1110-1144.
+__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8],
+                                       const uint64_t* __restrict__ T) {
+    uint64_t k[8], t[8], x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = h[i];
+    x[0] ^= n0;
+    gost_lps(k, x, T);                                   // K = LPS(h ^ N)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = k[i] ^ m[i];
+    gost_lps(t, x, T);                                   // t = LPS(K ^ m)
+    // Rounds 1..11: K = LPS(K ^ C_{r-1}); t = LPS(t ^ K).  Kept rolled: the
+    // body is 128 LDS lookups already, the constants are wave-uniform loads.
+#pragma unroll 1
+    for (int r = 0; r < 11; ++r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[r][i];
+        gost_lps(k, x, T);                               // K = LPS(K ^ C_r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = t[i] ^ k[i];
+        gost_lps(t, x, T);                               // t = LPS(t ^ K)
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[11][i];
+    gost_lps(k, x, T);                                   // K13 = LPS(K ^ C_11)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= m[i] ^ t[i] ^ k[i];  // :1142
+}
+
+template <bool k256>
+struct Gost {
+    static constexpr int kBlock = 64, kDigest = k256 ? 32 : 64, kWords = 16;
+    uint64_t h[8], n0, sg[8];
+    __device__ __forceinline__ void init() {  // gost3411-2012.h:1713-1729
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { h[i] = k256 ? 0x0101010101010101ull : 0ull; sg[i] = 0; }
+        n0 = 0;
+    }
+    // One g_N step over raw LE words w (gost3411-2012.h:1129-1131).
+    __device__ __forceinline__ void block(const uint32_t* w, uint64_t bits, const uint64_t* T) {
+        uint64_t m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+        gost_g(h, n0, m, T);
+        n0 += bits;
+        // Sigma += m mod 2^512 (gost3411-2012.h:996-1013).
+        uint32_t carry = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t s1 = sg[i] + m[i];
+            const uint32_t c1 = s1 < m[i];
+            const uint64_t s2 = s1 + carry;
+            carry = c1 | (s2 < s1);
+            sg[i] = s2;
+        }
+    }
+    // Tail + finalisation (gost3411-2012.h:1820-1839).
+    __device__ __forceinline__ void finish(uint32_t* w, uint32_t rem, const uint64_t* T) {
+        put_byte(w, rem, 0x01u);
+        block(w, (uint64_t)rem * 8u, T);
+        uint64_t m[8];
+        m[0] = n0;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m[i] = 0;
+        gost_g(h, 0, m, T);   // g_0(h, N)
+        gost_g(h, 0, sg, T);  // g_0(h, Sigma)
+    }
+    __device__ __forceinline__ void digest_words(uint32_t* out) const {
+        constexpr int first = 8 - kDigest / 8;  // last D bytes of h
+#pragma unroll
+        for (int i = 0; i < kDigest / 8; ++i) {
+            out[2 * i] = (uint32_t)h[first + i];
+            out[2 * i + 1] = (uint32_t)(h[first + i] >> 32);
+        }
+    }
+    __device__ __forceinline__ void save(uint32_t* p) const {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            p[2 * i] = (uint32_t)h[i]; p[2 * i + 1] = (uint32_t)(h[i] >> 32);
+            p[18 + 2 * i] = (uint32_t)sg[i]; p[19 + 2 * i] = (uint32_t)(sg[i] >> 32);
+        }
+        p[16] = (uint32_t)n0; p[17] = (uint32_t)(n0 >> 32);
+    }
+    __device__ __forceinline__ void load(const uint32_t* p) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            h[i] = (uint64_t)p[2 * i] | ((uint64_t)p[2 * i + 1] << 32);
+            sg[i] = (uint64_t)p[18 + 2 * i] | ((uint64_t)p[19 + 2 * i] << 32);
+        }
+        n0 = (uint64_t)p[16] | ((uint64_t)p[17] << 32);
+    }
+};
+
+// Whole message through a GOST state (gost3411_2012_update + _final).
+template <bool k256>
+__device__ __forceinline__ void gost_message(Gost<k256>& st, const uint8_t* msg, uint64_t len,
+                                             const uint64_t* T) {
+    uint32_t w[16];
+    const uint64_t nfull = len / 64;
+    const uint8_t* p = msg;
+    for (uint64_t b = 0; b < nfull; ++b, p += 64) {
+        load_full64(p, w);
+        st.block(w, 512, T);
+    }
+    const uint32_t rem = (uint32_t)(len - nfull * 64);
+    load_tail64(p, rem, w);
+    st.finish(w, rem, T);
+}
+
+}  // namespace lcbgpu

@@ -1,0 +1,489 @@
+// hash_device.hpp — per-lane compression functions and message drivers for
+// the MI355X (gfx950) batch digest kernels.
+//
+// Mapping: ONE LANE PER MESSAGE.  Merkle-Damgard (MD5/SHA) and Streebog chain
+// every block through the previous state, so the 64 lanes of a wavefront each
+// carry an independent message ("one wavefront per buffer" vs the
+// serial chain).  All state lives in VGPRs; rounds are fully unrolled with
+// compile-time indices so nothing spills to scratch.  The only memory traffic
+// is the message bytes (read once) and the digest (written once).
+//
+// Bit-exactness notes:
+//  * message words are loaded as raw little-endian u32; SHA policies byte-swap
+//    them (v_perm_b32) inside compress();
+//  * counts are bytes; bit length = bytes << 3 (md5.h:282, sha2.h:725-731);
+//  * GOST pads with 0x01 and never emits a length block
+//    (gost3411-2012.h:1820-1837).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lcbgpu {
+
+// ------------------------------------------------------------ primitives
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, 32u - n);  // v_alignbit_b32
+}
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, n);
+}
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t n) {
+    return (x >> n) | (x << (64u - n));
+}
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) {
+    return __builtin_amdgcn_perm(0u, x, 0x00010203u);  // v_perm_b32
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return a ^ b ^ c;  // v_xor3_b32
+}
+
+// ------------------------------------------------------- block loading
+// Bytes [p, p+64) of a message that has at least 64 bytes left, as 16 raw LE
+// words.  Any alignment.  Every dword loaded contains >= 1 message byte, so
+// no access leaves the buffer the caller described.
+__device__ __forceinline__ void load_full64(const uint8_t* p, uint32_t w[16]) {
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+    if ((ip & 15u) == 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = q[k];
+            w[4 * k + 0] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+    } else if ((ip & 3u) == 0) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = q[k];
+    } else {
+        const uint32_t sh = (uint32_t)(ip & 3u);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(ip - sh);
+        uint32_t d[17];
+#pragma unroll
+        for (int k = 0; k < 17; ++k) d[k] = q[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    }
+}
+
+// Bytes [p, p+rem) (0 <= rem < 64) as raw LE words; bytes >= rem are zero.
+__device__ __forceinline__ void load_tail64(const uint8_t* p, uint32_t rem, uint32_t w[16]) {
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(ip & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(ip - sh);
+    const uint32_t lim = rem + sh;  // aligned dword j holds a message byte iff 4j < lim
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) d[k] = (4u * k < lim) ? q[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const int valid = (int)rem - 4 * k;  // bytes of word k inside the message
+        const uint32_t mask = valid >= 4 ? 0xffffffffu
+                            : (valid <= 0 ? 0u : (0xffffffffu >> (32 - 8 * valid)));
+        w[k] = v & mask;
+    }
+}
+
+// OR byte value `b` into raw LE byte position `pos` (0..63) of w.
+__device__ __forceinline__ void put_byte(uint32_t w[16], uint32_t pos, uint32_t b) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        w[k] |= ((pos >> 2) == (uint32_t)k) ? (b << (8u * (pos & 3u))) : 0u;
+}
+
+// ================================================================== MD5
+// md5.h:137-229.  Round functions in their bitop3-friendly forms.
+struct Md5 {
+    static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16;
+    uint32_t s[4];
+    __device__ __forceinline__ void init() {
+        s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
+    }
+#define LCB_MD5_STEP(f, a, b, c, d, x, t, r) \
+    a = b + rotl32(a + (f) + (x) + (t), r)
+    __device__ __forceinline__ void compress(const uint32_t* w) {
+        uint32_t a = s[0], b = s[1], c = s[2], d = s[3];
+#define F1(b, c, d) (((c) ^ (d)) & (b)) ^ (d)
+#define F2(b, c, d) (((b) ^ (c)) & (d)) ^ (c)
+#define F3(b, c, d) ((b) ^ (c) ^ (d))
+#define F4(b, c, d) ((c) ^ ((b) | ~(d)))
+        LCB_MD5_STEP(F1(b, c, d), a, b, c, d, w[0], 0xd76aa478u, 7);
+        LCB_MD5_STEP(F1(a, b, c), d, a, b, c, w[1], 0xe8c7b756u, 12);
+        LCB_MD5_STEP(F1(d, a, b), c, d, a, b, w[2], 0x242070dbu, 17);
+        LCB_MD5_STEP(F1(c, d, a), b, c, d, a, w[3], 0xc1bdceeeu, 22);
+        LCB_MD5_STEP(F1(b, c, d), a, b, c, d, w[4], 0xf57c0fafu, 7);
+        LCB_MD5_STEP(F1(a, b, c), d, a, b, c, w[5], 0x4787c62au, 12);
+        LCB_MD5_STEP(F1(d, a, b), c, d, a, b, w[6], 0xa8304613u, 17);
+        LCB_MD5_STEP(F1(c, d, a), b, c, d, a, w[7], 0xfd469501u, 22);
+        LCB_MD5_STEP(F1(b, c, d), a, b, c, d, w[8], 0x698098d8u, 7);
+        LCB_MD5_STEP(F1(a, b, c), d, a, b, c, w[9], 0x8b44f7afu, 12);
+        LCB_MD5_STEP(F1(d, a, b), c, d, a, b, w[10], 0xffff5bb1u, 17);
+        LCB_MD5_STEP(F1(c, d, a), b, c, d, a, w[11], 0x895cd7beu, 22);
+        LCB_MD5_STEP(F1(b, c, d), a, b, c, d, w[12], 0x6b901122u, 7);
+        LCB_MD5_STEP(F1(a, b, c), d, a, b, c, w[13], 0xfd987193u, 12);
+        LCB_MD5_STEP(F1(d, a, b), c, d, a, b, w[14], 0xa679438eu, 17);
+        LCB_MD5_STEP(F1(c, d, a), b, c, d, a, w[15], 0x49b40821u, 22);
+
+        LCB_MD5_STEP(F2(b, c, d), a, b, c, d, w[1], 0xf61e2562u, 5);
+        LCB_MD5_STEP(F2(a, b, c), d, a, b, c, w[6], 0xc040b340u, 9);
+        LCB_MD5_STEP(F2(d, a, b), c, d, a, b, w[11], 0x265e5a51u, 14);
+        LCB_MD5_STEP(F2(c, d, a), b, c, d, a, w[0], 0xe9b6c7aau, 20);
+        LCB_MD5_STEP(F2(b, c, d), a, b, c, d, w[5], 0xd62f105du, 5);
+        LCB_MD5_STEP(F2(a, b, c), d, a, b, c, w[10], 0x02441453u, 9);
+        LCB_MD5_STEP(F2(d, a, b), c, d, a, b, w[15], 0xd8a1e681u, 14);
+        LCB_MD5_STEP(F2(c, d, a), b, c, d, a, w[4], 0xe7d3fbc8u, 20);
+        LCB_MD5_STEP(F2(b, c, d), a, b, c, d, w[9], 0x21e1cde6u, 5);
+        LCB_MD5_STEP(F2(a, b, c), d, a, b, c, w[14], 0xc33707d6u, 9);
+        LCB_MD5_STEP(F2(d, a, b), c, d, a, b, w[3], 0xf4d50d87u, 14);
+        LCB_MD5_STEP(F2(c, d, a), b, c, d, a, w[8], 0x455a14edu, 20);
+        LCB_MD5_STEP(F2(b, c, d), a, b, c, d, w[13], 0xa9e3e905u, 5);
+        LCB_MD5_STEP(F2(a, b, c), d, a, b, c, w[2], 0xfcefa3f8u, 9);
+        LCB_MD5_STEP(F2(d, a, b), c, d, a, b, w[7], 0x676f02d9u, 14);
+        LCB_MD5_STEP(F2(c, d, a), b, c, d, a, w[12], 0x8d2a4c8au, 20);
+
+        LCB_MD5_STEP(F3(b, c, d), a, b, c, d, w[5], 0xfffa3942u, 4);
+        LCB_MD5_STEP(F3(a, b, c), d, a, b, c, w[8], 0x8771f681u, 11);
+        LCB_MD5_STEP(F3(d, a, b), c, d, a, b, w[11], 0x6d9d6122u, 16);
+        LCB_MD5_STEP(F3(c, d, a), b, c, d, a, w[14], 0xfde5380cu, 23);
+        LCB_MD5_STEP(F3(b, c, d), a, b, c, d, w[1], 0xa4beea44u, 4);
+        LCB_MD5_STEP(F3(a, b, c), d, a, b, c, w[4], 0x4bdecfa9u, 11);
+        LCB_MD5_STEP(F3(d, a, b), c, d, a, b, w[7], 0xf6bb4b60u, 16);
+        LCB_MD5_STEP(F3(c, d, a), b, c, d, a, w[10], 0xbebfbc70u, 23);
+        LCB_MD5_STEP(F3(b, c, d), a, b, c, d, w[13], 0x289b7ec6u, 4);
+        LCB_MD5_STEP(F3(a, b, c), d, a, b, c, w[0], 0xeaa127fau, 11);
+        LCB_MD5_STEP(F3(d, a, b), c, d, a, b, w[3], 0xd4ef3085u, 16);
+        LCB_MD5_STEP(F3(c, d, a), b, c, d, a, w[6], 0x04881d05u, 23);
+        LCB_MD5_STEP(F3(b, c, d), a, b, c, d, w[9], 0xd9d4d039u, 4);
+        LCB_MD5_STEP(F3(a, b, c), d, a, b, c, w[12], 0xe6db99e5u, 11);
+        LCB_MD5_STEP(F3(d, a, b), c, d, a, b, w[15], 0x1fa27cf8u, 16);
+        LCB_MD5_STEP(F3(c, d, a), b, c, d, a, w[2], 0xc4ac5665u, 23);
+
+        LCB_MD5_STEP(F4(b, c, d), a, b, c, d, w[0], 0xf4292244u, 6);
+        LCB_MD5_STEP(F4(a, b, c), d, a, b, c, w[7], 0x432aff97u, 10);
+        LCB_MD5_STEP(F4(d, a, b), c, d, a, b, w[14], 0xab9423a7u, 15);
+        LCB_MD5_STEP(F4(c, d, a), b, c, d, a, w[5], 0xfc93a039u, 21);
+        LCB_MD5_STEP(F4(b, c, d), a, b, c, d, w[12], 0x655b59c3u, 6);
+        LCB_MD5_STEP(F4(a, b, c), d, a, b, c, w[3], 0x8f0ccc92u, 10);
+        LCB_MD5_STEP(F4(d, a, b), c, d, a, b, w[10], 0xffeff47du, 15);
+        LCB_MD5_STEP(F4(c, d, a), b, c, d, a, w[1], 0x85845dd1u, 21);
+        LCB_MD5_STEP(F4(b, c, d), a, b, c, d, w[8], 0x6fa87e4fu, 6);
+        LCB_MD5_STEP(F4(a, b, c), d, a, b, c, w[15], 0xfe2ce6e0u, 10);
+        LCB_MD5_STEP(F4(d, a, b), c, d, a, b, w[6], 0xa3014314u, 15);
+        LCB_MD5_STEP(F4(c, d, a), b, c, d, a, w[13], 0x4e0811a1u, 21);
+        LCB_MD5_STEP(F4(b, c, d), a, b, c, d, w[4], 0xf7537e82u, 6);
+        LCB_MD5_STEP(F4(a, b, c), d, a, b, c, w[11], 0xbd3af235u, 10);
+        LCB_MD5_STEP(F4(d, a, b), c, d, a, b, w[2], 0x2ad7d2bbu, 15);
+        LCB_MD5_STEP(F4(c, d, a), b, c, d, a, w[9], 0xeb86d391u, 21);
+#undef F1
+#undef F2
+#undef F3
+#undef F4
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d;
+    }
+#undef LCB_MD5_STEP
+    // md5.h:282: LE u64 bit length in bytes 56..63.
+    __device__ __forceinline__ static void put_length(uint32_t* w, uint64_t bytes) {
+        const uint64_t bits = bytes << 3;
+        w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32);
+    }
+    // md5.h:285: state bytes LE.
+    __device__ __forceinline__ void digest_words(uint32_t* out) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[i] = s[i];
+    }
+};
+
+// ================================================================ SHA-1
+// sha1.h:220-292 with a 16-word rolling schedule.
+struct Sha1 {
+    static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16;
+    uint32_t s[5];
+    __device__ __forceinline__ void init() {
+        s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
+        s[4] = 0xc3d2e1f0u;
+    }
+    __device__ __forceinline__ void compress(const uint32_t* raw) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = bswap32(raw[i]);
+        uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
+#pragma unroll
+        for (int i = 0; i < 80; ++i) {
+            uint32_t x;
+            if (i < 16) {
+                x = w[i];
+            } else {
+                x = rotl32(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15]) ^ w[i & 15], 1);
+                w[i & 15] = x;
+            }
+            uint32_t f, k;
+            if (i < 20) { f = ((c ^ d) & b) ^ d; k = 0x5a827999u; }
+            else if (i < 40) { f = xor3(b, c, d); k = 0x6ed9eba1u; }
+            else if (i < 60) { f = (b & c) | ((b | c) & d); k = 0x8f1bbcdcu; }
+            else { f = xor3(b, c, d); k = 0xca62c1d6u; }
+            const uint32_t t = rotl32(a, 5) + f + e + k + x;
+            e = d; d = c; c = rotl32(b, 30); b = a; a = t;
+        }
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e;
+    }
+    // sha1.h:833: BE u64 bit length.
+    __device__ __forceinline__ static void put_length(uint32_t* w, uint64_t bytes) {
+        const uint64_t bits = bytes << 3;
+        w[14] = bswap32((uint32_t)(bits >> 32)); w[15] = bswap32((uint32_t)bits);
+    }
+    // sha1.h:837: BE state.
+    __device__ __forceinline__ void digest_words(uint32_t* out) const {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) out[i] = bswap32(s[i]);
+    }
+};
+
+// ============================================================ SHA-224/256
+// sha2.h:260-327.
+__constant__ static const uint32_t kSha256K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+template <bool k224>
+struct Sha256 {
+    static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16;
+    uint32_t s[8];
+    __device__ __forceinline__ void init() {
+        if (k224) {  // sha2.h:129-132
+            s[0] = 0xc1059ed8u; s[1] = 0x367cd507u; s[2] = 0x3070dd17u; s[3] = 0xf70e5939u;
+            s[4] = 0xffc00b31u; s[5] = 0x68581511u; s[6] = 0x64f98fa7u; s[7] = 0xbefa4fa4u;
+        } else {     // sha2.h:134-137
+            s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
+            s[4] = 0x510e527fu; s[5] = 0x9b05688cu; s[6] = 0x1f83d9abu; s[7] = 0x5be0cd19u;
+        }
+    }
+    __device__ __forceinline__ void compress(const uint32_t* raw) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = bswap32(raw[i]);
+        uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            uint32_t x;
+            if (i < 16) {
+                x = w[i];
+            } else {
+                const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+                const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+                x = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+                w[i & 15] = x;
+            }
+            const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+            const uint32_t ch = ((f ^ g) & e) ^ g;
+            const uint32_t t1 = h + S1 + ch + kSha256K[i] + x;
+            const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+            const uint32_t mj = (a & b) | ((a | b) & c);
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+        }
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+    }
+    __device__ __forceinline__ static void put_length(uint32_t* w, uint64_t bytes) {
+        const uint64_t bits = bytes << 3;  // sha2.h:726
+        w[14] = bswap32((uint32_t)(bits >> 32)); w[15] = bswap32((uint32_t)bits);
+    }
+    __device__ __forceinline__ void digest_words(uint32_t* out) const {
+#pragma unroll
+        for (int i = 0; i < kDigest / 4; ++i) out[i] = bswap32(s[i]);  // sha2.h:735-736
+    }
+};
+
+// ============================================================ SHA-384/512
+// sha2.h:531-613; 64-bit words emulated on the 32-bit VALU (v_alignbit pairs,
+// v_add_co/addc or v_lshl_add_u64).  Raw words: 32 LE u32 per 128-B block.
+__constant__ static const uint64_t kSha512K[80] = {
+    0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+    0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+    0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+    0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+    0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+    0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+    0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+    0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+    0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+    0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+    0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+    0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+    0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+    0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+    0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+    0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+    0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+    0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+    0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+    0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
+
+template <bool k384>
+struct Sha512 {
+    static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32;
+    uint64_t s[8];
+    __device__ __forceinline__ void init() {
+        if (k384) {  // sha2.h:139-143
+            s[0] = 0xcbbb9d5dc1059ed8ull; s[1] = 0x629a292a367cd507ull; s[2] = 0x9159015a3070dd17ull;
+            s[3] = 0x152fecd8f70e5939ull; s[4] = 0x67332667ffc00b31ull; s[5] = 0x8eb44a8768581511ull;
+            s[6] = 0xdb0c2e0d64f98fa7ull; s[7] = 0x47b5481dbefa4fa4ull;
+        } else {     // sha2.h:144-148
+            s[0] = 0x6a09e667f3bcc908ull; s[1] = 0xbb67ae8584caa73bull; s[2] = 0x3c6ef372fe94f82bull;
+            s[3] = 0xa54ff53a5f1d36f1ull; s[4] = 0x510e527fade682d1ull; s[5] = 0x9b05688c2b3e6c1full;
+            s[6] = 0x1f83d9abfb41bd6bull; s[7] = 0x5be0cd19137e2179ull;
+        }
+    }
+    __device__ __forceinline__ void compress(const uint32_t* raw) {
+        uint64_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            w[i] = ((uint64_t)bswap32(raw[2 * i]) << 32) | bswap32(raw[2 * i + 1]);  // sha2.h:582
+        uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+        for (int i = 0; i < 80; ++i) {
+            uint64_t x;
+            if (i < 16) {
+                x = w[i];
+            } else {
+                const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+                const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+                const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+                x = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+                w[i & 15] = x;
+            }
+            const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+            const uint64_t ch = ((f ^ g) & e) ^ g;
+            const uint64_t t1 = h + S1 + ch + kSha512K[i] + x;
+            const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+            const uint64_t mj = (a & b) | ((a | b) & c);
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+        }
+        s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+    }
+    // sha2.h:727-730: 128-bit BE bit length in bytes 112..127 (hi 64 bits =
+    // bytes >> 61 for any length below 2^64 bytes).
+    __device__ __forceinline__ static void put_length(uint32_t* w, uint64_t bytes) {
+        const uint64_t lo = bytes << 3, hi = bytes >> 61;
+        w[28] = bswap32((uint32_t)(hi >> 32)); w[29] = bswap32((uint32_t)hi);
+        w[30] = bswap32((uint32_t)(lo >> 32)); w[31] = bswap32((uint32_t)lo);
+    }
+    __device__ __forceinline__ void digest_words(uint32_t* out) const {  // sha2.h:738
+#pragma unroll
+        for (int i = 0; i < kDigest / 8; ++i) {
+            out[2 * i] = bswap32((uint32_t)(s[i] >> 32));
+            out[2 * i + 1] = bswap32((uint32_t)s[i]);
+        }
+    }
+};
+
+// HMAC mid-state save/load (state words only; the prefix length is implied).
+template <int N>
+__device__ __forceinline__ void save_words(const uint32_t (&s)[N], uint32_t* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = s[i];
+}
+template <int N>
+__device__ __forceinline__ void save_words(const uint64_t (&s)[N], uint32_t* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) { p[2 * i] = (uint32_t)s[i]; p[2 * i + 1] = (uint32_t)(s[i] >> 32); }
+}
+template <int N>
+__device__ __forceinline__ void load_words(uint32_t (&s)[N], const uint32_t* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = p[i];
+}
+template <int N>
+__device__ __forceinline__ void load_words(uint64_t (&s)[N], const uint32_t* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = (uint64_t)p[2 * i] | ((uint64_t)p[2 * i + 1] << 32);
+}
+
+// ------------------------------------------------- MD-family message driver
+// Loads block `blk` (kBlock bytes) of a message with `avail` >= kBlock bytes.
+template <class H>
+__device__ __forceinline__ void load_block_full(const uint8_t* p, uint32_t* w) {
+#pragma unroll
+    for (int h = 0; h < H::kBlock / 64; ++h) load_full64(p + 64 * h, w + 16 * h);
+}
+// Tail block: rem (< kBlock) message bytes, zero fill.
+template <class H>
+__device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, uint32_t* w) {
+#pragma unroll
+    for (int h = 0; h < H::kBlock / 64; ++h) {
+        const int r = (int)rem - 64 * h;
+        if (r >= 64) {
+            load_full64(p + 64 * h, w + 16 * h);
+        } else if (r > 0) {
+            load_tail64(p + 64 * h, (uint32_t)r, w + 16 * h);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[16 * h + k] = 0u;
+        }
+    }
+}
+
+// Processes a whole message of `len` bytes starting from state `st`, whose
+// compressed prefix is `prefix` bytes long (0, or the block for HMAC inner),
+// then pads (md5.h:266-288 / sha1.h:816-840 / sha2.h:706-742).
+template <class H>
+__device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
+    uint32_t w[H::kWords];
+    const uint64_t nfull = len / H::kBlock;
+    const uint8_t* p = msg;
+    for (uint64_t b = 0; b < nfull; ++b, p += H::kBlock) {
+        load_block_full<H>(p, w);
+        st.compress(w);
+    }
+    const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
+    load_block_tail<H>(p, rem, w);
+    // 0x80 terminator at byte `rem` (of a 64- or 128-byte block).
+#pragma unroll
+    for (int h = 0; h < H::kBlock / 64; ++h)
+        if ((rem >> 6) == (uint32_t)h) put_byte(w + 16 * h, rem & 63u, 0x80u);
+    if (rem + 1 + H::kLenBytes > (uint32_t)H::kBlock) {  // no room for the length
+        st.compress(w);
+#pragma unroll
+        for (int k = 0; k < H::kWords; ++k) w[k] = 0u;
+    }
+    H::put_length(w, len + prefix);
+    st.compress(w);
+}
+
+// Outer HMAC pass over an inner digest held in registers (digest words are
+// raw LE byte order): one block = digest || 0x80 || zeros || length(B + D).
+template <class H>
+__device__ __forceinline__ void md_outer(H& st, const uint32_t* dig) {
+    uint32_t w[H::kWords];
+#pragma unroll
+    for (int k = 0; k < H::kWords; ++k) w[k] = (k < H::kDigest / 4) ? dig[k] : 0u;
+    w[H::kDigest / 4] = 0x80u;  // D is a multiple of 4: terminator starts a fresh word
+    H::put_length(w, (uint64_t)H::kBlock + H::kDigest);
+    st.compress(w);
+}
+
+// Stores D digest bytes (raw LE word order) at out (any alignment).
+template <int D>
+__device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t* dw) {
+    if ((reinterpret_cast<uintptr_t>(out) & 3u) == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(out);
+        if ((D % 16) == 0 && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+#pragma unroll
+            for (int i = 0; i < D / 16; ++i)
+                reinterpret_cast<uint4*>(out)[i] = make_uint4(dw[4 * i], dw[4 * i + 1], dw[4 * i + 2], dw[4 * i + 3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < D / 4; ++i) o[i] = dw[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < D; ++i) out[i] = (uint8_t)(dw[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
+}  // namespace lcbgpu

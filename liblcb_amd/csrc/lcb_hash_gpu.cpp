@@ -1,0 +1,399 @@
+// lcb_hash_gpu.cpp — the exported C-ABI (include/lcb_hash_gpu.h).
+//
+// Device mode enqueues on the caller's stream and never synchronises (except
+// to stage a long HMAC key, see hmac_setup).  Host mode runs a double-buffered
+// pipeline on two private streams: pinned staging -> hipMemcpyAsync H2D ->
+// kernel -> hipMemcpyAsync D2H, chunk c+1's upload overlapping chunk c's
+// kernel.  Every HIP failure maps to an errno code; nothing falls back to the
+// CPU.
+#include <errno.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/lcb_hash_gpu.h"
+#include "lcb_internal.hpp"
+
+using namespace lcbgpu;
+
+namespace {
+
+size_t dsize(int alg) {
+    static const size_t ds[9] = {0, 16, 20, 28, 32, 48, 64, 32, 64};
+    return (alg >= 1 && alg <= 8) ? ds[alg] : 0;
+}
+size_t bsize(int alg) {
+    if (alg < 1 || alg > 8) return 0;
+    return (alg == LCB_HASH_SHA384 || alg == LCB_HASH_SHA512) ? 128 : 64;
+}
+
+int map_err(hipError_t e) {
+    switch (e) {
+    case hipSuccess: return 0;
+    case hipErrorOutOfMemory: return ENOMEM;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+    case hipErrorInsufficientDriver: return ENODEV;
+    default: return EIO;
+    }
+}
+
+#define LCB_TRY(expr)                        \
+    do {                                     \
+        hipError_t _e = (expr);              \
+        if (_e != hipSuccess) return map_err(_e); \
+    } while (0)
+
+// HMAC: build the key block / long-key buffer and enqueue the mid-state prep
+// kernel.  *mid receives a stream-ordered allocation the caller frees with
+// hipFreeAsync after the batch kernel.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
+               uint8_t** dkey_out) {
+    KeyBlock kb;
+    memset(&kb, 0, sizeof(kb));
+    uint8_t* dkey = nullptr;
+    const size_t B = bsize(alg);
+    if (key_len <= B) {
+        if (key_len) memcpy(kb.w, key, key_len);
+    } else {
+        // Long key: hashed on the device.  The copy is waited for so the
+        // caller may release `key` on return (pageable source memory).
+        LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&dkey), key_len, s));
+        LCB_TRY(hipMemcpyAsync(dkey, key, key_len, hipMemcpyHostToDevice, s));
+        LCB_TRY(hipStreamSynchronize(s));
+    }
+    LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(mid), 2 * kMidWords * sizeof(uint32_t), s));
+    launch_hmac_prep(alg, kb, dkey, key_len, *mid, s);
+    LCB_TRY(hipGetLastError());
+    *dkey_out = dkey;
+    return 0;
+}
+
+int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
+                 const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s) {
+    KArgs a;
+    a.data = data; a.offsets = offsets; a.lengths = lengths; a.order = nullptr;
+    a.count = count; a.stride = stride; a.fixed_len = fixed_len; a.digests = digests;
+    a.mid = nullptr;
+    uint32_t* mid = nullptr;
+    uint8_t* dkey = nullptr;
+    if (key) {
+        int rc = hmac_setup(alg, key, key_len, s, &mid, &dkey);
+        if (rc) return rc;
+        a.mid = mid;
+    }
+    launch_batch(alg, a, s);
+    hipError_t e = hipGetLastError();
+    if (mid) (void)hipFreeAsync(mid, s);
+    if (dkey) (void)hipFreeAsync(dkey, s);
+    return map_err(e);
+}
+
+// ------------------------------------------------------------ host mode
+// Per-thread staging context for the current device.
+struct Stage {
+    int device = -1;
+    size_t cap = 0;                 // data bytes per buffer
+    size_t mcap = 0;                // messages per buffer
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    uint8_t* h_data[2] = {nullptr, nullptr};
+    uint64_t* h_off[2] = {nullptr, nullptr};
+    uint32_t* h_len[2] = {nullptr, nullptr};
+    uint8_t* h_dig[2] = {nullptr, nullptr};
+    uint8_t* d_data[2] = {nullptr, nullptr};
+    uint64_t* d_off[2] = {nullptr, nullptr};
+    uint32_t* d_len[2] = {nullptr, nullptr};
+    uint8_t* d_dig[2] = {nullptr, nullptr};
+    // pending chunk per buffer (digests to copy out once `done` fires)
+    size_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
+    bool busy[2] = {false, false};
+
+    void release() {
+        for (int b = 0; b < 2; ++b) {
+            if (h_data[b]) (void)hipHostFree(h_data[b]);
+            if (h_off[b]) (void)hipHostFree(h_off[b]);
+            if (h_len[b]) (void)hipHostFree(h_len[b]);
+            if (h_dig[b]) (void)hipHostFree(h_dig[b]);
+            if (d_data[b]) (void)hipFree(d_data[b]);
+            if (d_off[b]) (void)hipFree(d_off[b]);
+            if (d_len[b]) (void)hipFree(d_len[b]);
+            if (d_dig[b]) (void)hipFree(d_dig[b]);
+            if (done[b]) (void)hipEventDestroy(done[b]);
+            if (st[b]) (void)hipStreamDestroy(st[b]);
+            h_data[b] = nullptr; h_off[b] = nullptr; h_len[b] = nullptr; h_dig[b] = nullptr;
+            d_data[b] = nullptr; d_off[b] = nullptr; d_len[b] = nullptr; d_dig[b] = nullptr;
+            done[b] = nullptr; st[b] = nullptr;
+        }
+        cap = mcap = 0;
+        device = -1;
+    }
+    ~Stage() { release(); }
+
+    int ensure(int dev, size_t need_bytes, size_t need_msgs) {
+        if (device == dev && cap >= need_bytes && mcap >= need_msgs) return 0;
+        size_t nb = std::max(need_bytes, cap), nm = std::max(need_msgs, mcap);
+        release();
+        device = dev;
+        for (int b = 0; b < 2; ++b) {
+            LCB_TRY(hipStreamCreateWithFlags(&st[b], hipStreamNonBlocking));
+            LCB_TRY(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+            LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_data[b]), nb, hipHostMallocDefault));
+            LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_off[b]), nm * 8, hipHostMallocDefault));
+            LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_len[b]), nm * 4, hipHostMallocDefault));
+            LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_dig[b]), nm * 64, hipHostMallocDefault));
+            LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_data[b]), nb));
+            LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_off[b]), nm * 8));
+            LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_len[b]), nm * 4));
+            LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_dig[b]), nm * 64));
+        }
+        cap = nb;
+        mcap = nm;
+        return 0;
+    }
+};
+
+thread_local Stage g_stage;
+constexpr size_t kChunkBytes = 64ull << 20;   // 64 MiB per in-flight chunk
+constexpr size_t kChunkMsgs = 1u << 18;       // 256 K messages per chunk
+
+int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
+               const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
+               uint32_t fixed_len, uint8_t* digests) {
+    int dev = 0;
+    LCB_TRY(hipGetDevice(&dev));
+    const size_t D = dsize(alg);
+    auto off_of = [&](size_t i) -> uint64_t { return offsets ? offsets[i] : (uint64_t)i * stride; };
+    auto len_of = [&](size_t i) -> uint64_t { return lengths ? lengths[i] : fixed_len; };
+
+    // Largest single message decides the minimum buffer.
+    uint64_t maxlen = 0;
+    if (lengths) {
+        for (size_t i = 0; i < count; ++i) maxlen = std::max<uint64_t>(maxlen, lengths[i]);
+    } else {
+        maxlen = fixed_len;
+    }
+    int rc = g_stage.ensure(dev, std::max<size_t>(kChunkBytes, maxlen), kChunkMsgs);
+    if (rc) return rc;
+    Stage& S = g_stage;
+
+    uint32_t* mid = nullptr;
+    uint8_t* dkey = nullptr;
+    if (key) {
+        rc = hmac_setup(alg, key, key_len, S.st[0], &mid, &dkey);
+        if (rc) return rc;
+        LCB_TRY(hipStreamSynchronize(S.st[0]));   // mid-states visible to both streams
+    }
+
+    auto drain = [&](int b) -> int {
+        if (!S.busy[b]) return 0;
+        LCB_TRY(hipEventSynchronize(S.done[b]));
+        memcpy(digests + S.pend_first[b] * D, S.h_dig[b], S.pend_n[b] * D);
+        S.busy[b] = false;
+        return 0;
+    };
+
+    size_t i = 0;
+    int b = 0;
+    while (i < count) {
+        if ((rc = drain(b))) break;
+        // Gather a chunk of messages [i, j) whose bytes fit the staging buffer.
+        size_t j = i, bytes = 0;
+        while (j < count && j - i < S.mcap) {
+            const uint64_t n = len_of(j);
+            if (bytes + n > S.cap && j > i) break;
+            memcpy(S.h_data[b] + bytes, data + off_of(j), n);
+            S.h_off[b][j - i] = bytes;
+            S.h_len[b][j - i] = (uint32_t)n;
+            bytes += n;
+            ++j;
+        }
+        const size_t n = j - i;
+        hipStream_t s = S.st[b];
+        if (hipMemcpyAsync(S.d_data[b], S.h_data[b], bytes ? bytes : 1, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(S.d_off[b], S.h_off[b], n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(S.d_len[b], S.h_len[b], n * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = EIO;
+            break;
+        }
+        KArgs a;
+        a.data = S.d_data[b]; a.offsets = S.d_off[b]; a.lengths = S.d_len[b]; a.order = nullptr;
+        a.count = n; a.stride = 0; a.fixed_len = 0; a.digests = S.d_dig[b]; a.mid = mid;
+        launch_batch(alg, a, s);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(S.h_dig[b], S.d_dig[b], n * D, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(S.done[b], s) != hipSuccess) {
+            rc = EIO;
+            break;
+        }
+        S.pend_first[b] = i;
+        S.pend_n[b] = n;
+        S.busy[b] = true;
+        i = j;
+        b ^= 1;
+    }
+    int rc2 = drain(0);
+    int rc3 = drain(1);
+    if (mid || dkey) {  // both streams are drained: release the HMAC state
+        if (mid) (void)hipFreeAsync(mid, S.st[0]);
+        if (dkey) (void)hipFreeAsync(dkey, S.st[0]);
+        (void)hipStreamSynchronize(S.st[0]);
+    }
+    if (rc) return rc;
+    if (rc2) return rc2;
+    return rc3;
+}
+
+std::once_flag g_init_flag;
+int g_init_rc = 0;
+
+}  // namespace
+
+// ================================================================== ABI
+extern "C" {
+
+int lcb_hash_gpu_abi_version(void) { return LCB_HASH_GPU_ABI_VERSION; }
+size_t lcb_hash_digest_size(int alg) { return dsize(alg); }
+size_t lcb_hash_block_size(int alg) { return bsize(alg); }
+
+int lcb_hash_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* lcb_hash_strerror(int error) {
+    switch (error) {
+    case 0: return "success";
+    case EINVAL: return "invalid argument";
+    case ENOMEM: return "out of device or pinned memory";
+    case ENODEV: return "no usable MI355X / HIP device";
+    case EIO: return "HIP launch or copy failure";
+    default: return "unknown error";
+    }
+}
+
+int lcb_hash_batch(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
+                   const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
+                   uint32_t fixed_len, uint8_t* digests, uint32_t flags, void* stream) {
+    if (dsize(alg) == 0) return EINVAL;
+    if (flags & ~LCB_HASH_F_DEVICE) return EINVAL;
+    if (count == 0) return 0;
+    if (!data || !digests) return EINVAL;
+    if (key == nullptr && key_len != 0) return EINVAL;
+    std::call_once(g_init_flag, [] {
+        int n = 0;
+        g_init_rc = (hipGetDeviceCount(&n) != hipSuccess || n <= 0) ? ENODEV : 0;
+    });
+    if (g_init_rc) return g_init_rc;
+    if (flags & LCB_HASH_F_DEVICE)
+        return batch_device(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len,
+                            digests, reinterpret_cast<hipStream_t>(stream));
+    return batch_host(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len, digests);
+}
+
+int md5_get_digest_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                         size_t count, uint64_t stride, uint32_t fixed_len, uint8_t* digests,
+                         uint32_t flags, void* stream) {
+    return lcb_hash_batch(LCB_HASH_MD5, nullptr, 0, data, offsets, lengths, count, stride, fixed_len,
+                          digests, flags, stream);
+}
+int md5_hmac_get_digest_batch(const uint8_t* key, size_t key_size, const uint8_t* data,
+                              const uint64_t* offsets, const uint32_t* lengths, size_t count,
+                              uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags,
+                              void* stream) {
+    static const uint8_t empty = 0;
+    return lcb_hash_batch(LCB_HASH_MD5, key ? key : &empty, key_size, data, offsets, lengths, count,
+                          stride, fixed_len, digests, flags, stream);
+}
+int sha1_get_digest_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                          size_t count, uint64_t stride, uint32_t fixed_len, uint8_t* digests,
+                          uint32_t flags, void* stream) {
+    return lcb_hash_batch(LCB_HASH_SHA1, nullptr, 0, data, offsets, lengths, count, stride, fixed_len,
+                          digests, flags, stream);
+}
+int sha1_hmac_get_digest_batch(const uint8_t* key, size_t key_size, const uint8_t* data,
+                               const uint64_t* offsets, const uint32_t* lengths, size_t count,
+                               uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags,
+                               void* stream) {
+    static const uint8_t empty = 0;
+    return lcb_hash_batch(LCB_HASH_SHA1, key ? key : &empty, key_size, data, offsets, lengths, count,
+                          stride, fixed_len, digests, flags, stream);
+}
+
+// sha2_init's bits convention (sha2.h:217-241): bits or bytes.
+static int sha2_alg(size_t bits) {
+    switch (bits) {
+    case 224: case 28: return LCB_HASH_SHA224;
+    case 256: case 32: return LCB_HASH_SHA256;
+    case 384: case 48: return LCB_HASH_SHA384;
+    case 512: case 64: return LCB_HASH_SHA512;
+    }
+    return 0;
+}
+// gost3411_2012_init (gost3411-2012.h:1715-1729): 256/32 -> 256, else 512.
+static int gost_alg(size_t bits) {
+    return (bits == 256 || bits == 32) ? LCB_HASH_GOST256 : LCB_HASH_GOST512;
+}
+
+int sha2_get_digest_batch(size_t bits, const uint8_t* data, const uint64_t* offsets,
+                          const uint32_t* lengths, size_t count, uint64_t stride, uint32_t fixed_len,
+                          uint8_t* digests, size_t* digest_size, uint32_t flags, void* stream) {
+    const int alg = sha2_alg(bits);
+    if (!alg) return EINVAL;
+    if (digest_size) *digest_size = dsize(alg);
+    return lcb_hash_batch(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
+                          flags, stream);
+}
+int sha2_hmac_get_digest_batch(size_t bits, const uint8_t* key, size_t key_size, const uint8_t* data,
+                               const uint64_t* offsets, const uint32_t* lengths, size_t count,
+                               uint64_t stride, uint32_t fixed_len, uint8_t* digests,
+                               size_t* digest_size, uint32_t flags, void* stream) {
+    static const uint8_t empty = 0;
+    const int alg = sha2_alg(bits);
+    if (!alg) return EINVAL;
+    if (digest_size) *digest_size = dsize(alg);
+    return lcb_hash_batch(alg, key ? key : &empty, key_size, data, offsets, lengths, count, stride,
+                          fixed_len, digests, flags, stream);
+}
+int gost3411_2012_get_digest_batch(size_t bits, const uint8_t* data, const uint64_t* offsets,
+                                   const uint32_t* lengths, size_t count, uint64_t stride,
+                                   uint32_t fixed_len, uint8_t* digests, size_t* digest_size,
+                                   uint32_t flags, void* stream) {
+    const int alg = gost_alg(bits);
+    if (digest_size) *digest_size = dsize(alg);
+    return lcb_hash_batch(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
+                          flags, stream);
+}
+int gost3411_2012_hmac_get_digest_batch(size_t bits, const uint8_t* key, size_t key_size,
+                                        const uint8_t* data, const uint64_t* offsets,
+                                        const uint32_t* lengths, size_t count, uint64_t stride,
+                                        uint32_t fixed_len, uint8_t* digests, size_t* digest_size,
+                                        uint32_t flags, void* stream) {
+    static const uint8_t empty = 0;
+    const int alg = gost_alg(bits);
+    if (digest_size) *digest_size = dsize(alg);
+    return lcb_hash_batch(alg, key ? key : &empty, key_size, data, offsets, lengths, count, stride,
+                          fixed_len, digests, flags, stream);
+}
+
+int lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t* dev_out, size_t n, void* stream) {
+    if (n == 0) return 0;
+    if (!dev_out) return EINVAL;
+    launch_gen(seed, start, dev_out, n, reinterpret_cast<hipStream_t>(stream));
+    return map_err(hipGetLastError());
+}
+
+int lcb_hash_gpu_gost_table(uint64_t* out) {
+    if (!out) return EINVAL;
+    gost_table_host(out);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,35 @@
+// lcb_internal.hpp — types shared by the kernel TU and the C-ABI TU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lcbgpu {
+
+// Device-side description of one batch (see include/lcb_hash_gpu.h).
+struct KArgs {
+    const uint8_t* data;
+    const uint64_t* offsets;   // nullptr: i * stride
+    const uint32_t* lengths;   // nullptr: fixed_len
+    const uint32_t* order;     // nullptr: identity; else bucketing permutation
+    uint64_t count;
+    uint64_t stride;
+    uint32_t fixed_len;
+    uint8_t* digests;          // packed count x D
+    const uint32_t* mid;       // HMAC mid-states (nullptr: plain digest)
+};
+
+// Words reserved per HMAC mid-state (GOST needs 34: h, N, Sigma).
+constexpr int kMidWords = 64;
+
+// Short HMAC key, zero padded to 128 bytes, passed by value.
+struct KeyBlock {
+    uint32_t w[32];
+};
+
+void launch_batch(int alg, const KArgs& a, hipStream_t s);
+void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
+                      uint32_t* mid, hipStream_t s);
+void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
+void gost_table_host(uint64_t* out);
+
+}  // namespace lcbgpu

@@ -1,0 +1,233 @@
+// lcb_kernels.hip — MI355X (gfx950) batch digest kernels and their launchers.
+//
+// Grid: one lane per message, 256-thread workgroups (4 waves), message index
+// = blockIdx.x * 256 + threadIdx.x, optionally through a bucketing
+// permutation `order` (ragged batches: similar lengths share a wavefront).
+// No inter-workgroup communication; every message is independent.
+#include <hip/hip_runtime.h>
+#include "hash_device.hpp"
+#include "gost_device.hpp"
+#include "lcb_internal.hpp"
+
+namespace lcbgpu {
+
+__device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.count) return false;
+    idx = a.order ? (uint64_t)a.order[i] : i;
+    msg = a.data + (a.offsets ? a.offsets[idx] : idx * a.stride);
+    len = a.lengths ? (uint64_t)a.lengths[idx] : (uint64_t)a.fixed_len;
+    return true;
+}
+
+// ------------------------------------------------------------- MD family
+template <class H, bool kHmac>
+__global__ __launch_bounds__(256) void md_batch_kernel(KArgs a) {
+    uint64_t idx, len;
+    const uint8_t* msg;
+    if (!msg_at(a, idx, msg, len)) return;
+    H st;
+    uint32_t dw[H::kDigest / 4];
+    if (kHmac) {
+        load_words(st.s, a.mid);                       // state after K ^ ipad
+        md_message(st, msg, len, (uint64_t)H::kBlock);
+        st.digest_words(dw);
+        H o;
+        load_words(o.s, a.mid + kMidWords);            // state after K ^ opad
+        md_outer(o, dw);
+        o.digest_words(dw);
+    } else {
+        st.init();
+        md_message(st, msg, len, 0);
+        st.digest_words(dw);
+    }
+    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
+}
+
+// HMAC key schedule on the device (RFC 2104, md5.h:309-338): key block =
+// key (<= B bytes, passed by value) or H(key) (long key in device memory);
+// mid[0..] = state after (K ^ ipad), mid[kMidWords..] = state after (K ^ opad).
+template <class H>
+__global__ void md_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t k[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) k[i] = kb.w[i];
+    if (dkey) {
+        H st;
+        st.init();
+        md_message(st, dkey, key_len, 0);
+        uint32_t dw[H::kDigest / 4];
+        st.digest_words(dw);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) k[i] = (i < H::kDigest / 4) ? dw[i] : 0u;
+    }
+    uint32_t w[H::kWords];
+    H st;
+#pragma unroll
+    for (int i = 0; i < H::kWords; ++i) w[i] = k[i] ^ 0x36363636u;
+    st.init();
+    st.compress(w);
+    save_words(st.s, mid);
+#pragma unroll
+    for (int i = 0; i < H::kWords; ++i) w[i] = k[i] ^ 0x5c5c5c5cu;
+    st.init();
+    st.compress(w);
+    save_words(st.s, mid + kMidWords);
+}
+
+// ------------------------------------------------------------------ GOST
+template <bool k256, bool kHmac>
+__global__ __launch_bounds__(256) void gost_batch_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint64_t T[8 * 256];
+    gost_stage_table(T);
+    uint64_t idx, len;
+    const uint8_t* msg;
+    if (!msg_at(a, idx, msg, len)) return;
+    using G = Gost<k256>;
+    G st;
+    uint32_t dw[G::kDigest / 4];
+    if (kHmac) {
+        st.load(a.mid);
+        gost_message(st, msg, len, T);
+        st.digest_words(dw);
+        // Outer pass: fresh state after K ^ opad, message = inner digest.
+        G o;
+        o.load(a.mid + kMidWords);
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
+        if (G::kDigest == 64) {       // a 64-byte digest is a full block, then an
+            o.block(w, 512, T);       // empty pad block (gost3411-2012.h:1783-1793)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = 0u;
+            o.finish(w, 0, T);
+        } else {
+            o.finish(w, G::kDigest, T);  // 32 bytes: the digest is the tail block
+        }
+        o.digest_words(dw);
+    } else {
+        st.init();
+        gost_message(st, msg, len, T);
+        st.digest_words(dw);
+    }
+    store_digest<G::kDigest>(a.digests + idx * G::kDigest, dw);
+}
+
+template <bool k256>
+__global__ void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid) {
+    __shared__ __attribute__((aligned(16))) uint64_t T[8 * 256];
+    gost_stage_table(T);
+    if (threadIdx.x != 0) return;
+    using G = Gost<k256>;
+    uint32_t k[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = kb.w[i];
+    if (dkey) {  // gost3411-2012.h:1873-1878: long key -> its digest
+        G st;
+        st.init();
+        gost_message(st, dkey, key_len, T);
+        uint32_t dw[G::kDigest / 4];
+        st.digest_words(dw);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) k[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
+    }
+    uint32_t w[16];
+    G st;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x36363636u;
+    st.init();
+    st.block(w, 512, T);
+    st.save(mid);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x5c5c5c5cu;
+    st.init();
+    st.block(w, 512, T);
+    st.save(mid + kMidWords);
+}
+
+// ------------------------------------------------------ synthetic input
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// Thread t writes stream word (start/8 + t) — the bytes of it that fall in
+// [start, start + n) — to out[word*8 - start ...].
+__global__ __launch_bounds__(256) void gen_kernel(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n) {
+    const uint64_t w0 = start >> 3;
+    const uint64_t nw = ((start + n + 7) >> 3) - w0;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nw;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t word = w0 + t;
+        const uint64_t v = mix64(seed ^ word);
+        const uint64_t b0 = word << 3;
+        if (b0 >= start && b0 + 8 <= start + n && ((reinterpret_cast<uintptr_t>(out + (b0 - start)) & 7u) == 0)) {
+            *reinterpret_cast<uint64_t*>(out + (b0 - start)) = v;
+        } else {
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t b = b0 + k;
+                if (b >= start && b < start + n) out[b - start] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- launchers
+static inline dim3 grid_for(uint64_t count) { return dim3((unsigned)((count + 255) / 256)); }
+
+template <class H>
+static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
+    if (hmac) hipLaunchKernelGGL((md_batch_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((md_batch_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
+}
+template <bool k256>
+static void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
+    if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), grid_for(a.count), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), grid_for(a.count), dim3(256), 0, s, a);
+}
+
+void launch_batch(int alg, const KArgs& a, hipStream_t s) {
+    const bool hmac = a.mid != nullptr;
+    switch (alg) {
+    case 1: launch_md<Md5>(a, hmac, s); break;
+    case 2: launch_md<Sha1>(a, hmac, s); break;
+    case 3: launch_md<Sha256<true>>(a, hmac, s); break;
+    case 4: launch_md<Sha256<false>>(a, hmac, s); break;
+    case 5: launch_md<Sha512<true>>(a, hmac, s); break;
+    case 6: launch_md<Sha512<false>>(a, hmac, s); break;
+    case 7: launch_gost<true>(a, hmac, s); break;
+    case 8: launch_gost<false>(a, hmac, s); break;
+    }
+}
+
+void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
+                      uint32_t* mid, hipStream_t s) {
+    switch (alg) {
+    case 1: hipLaunchKernelGGL(md_hmac_prep_kernel<Md5>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 2: hipLaunchKernelGGL(md_hmac_prep_kernel<Sha1>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 3: hipLaunchKernelGGL(md_hmac_prep_kernel<Sha256<true>>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 4: hipLaunchKernelGGL(md_hmac_prep_kernel<Sha256<false>>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 5: hipLaunchKernelGGL(md_hmac_prep_kernel<Sha512<true>>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 6: hipLaunchKernelGGL(md_hmac_prep_kernel<Sha512<false>>, dim3(1), dim3(64), 0, s, kb, dkey, key_len, mid); break;
+    case 7: hipLaunchKernelGGL(gost_hmac_prep_kernel<true>, dim3(1), dim3(256), 0, s, kb, dkey, key_len, mid); break;
+    case 8: hipLaunchKernelGGL(gost_hmac_prep_kernel<false>, dim3(1), dim3(256), 0, s, kb, dkey, key_len, mid); break;
+    }
+}
+
+void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s) {
+    const uint64_t nw = ((start + n + 7) >> 3) - (start >> 3);
+    uint64_t blocks = (nw + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(256), 0, s, seed, start, out, n);
+}
+
+void gost_table_host(uint64_t* out) {
+    for (int j = 0; j < 8; ++j)
+        for (int b = 0; b < 256; ++b) out[j * 256 + b] = kGostAxHost.t[j][b];
+}
+
+}  // namespace lcbgpu

@@ -1,0 +1,172 @@
+"""Host-side mirror of liblcb's include/crypto/hash one-shot API, batched.
+
+Each function below is the batch counterpart of the reference function named
+in its docstring and returns, per message, exactly the bytes that function
+writes.  Arguments keep the reference's meaning (`bits` as sha2_init /
+gost3411_2012_init, `key`/`key_size` as the *_hmac_* functions); the batch
+adds the buffer description of include/lcb_hash_gpu.h.
+
+Memory modes
+  * torch CUDA (ROCm) tensors -> device mode: the kernels run on the tensor's
+    device, enqueued on torch's current stream; the call does not synchronise.
+  * numpy arrays / bytes      -> host mode: pinned staging, H2D, kernel, D2H.
+
+Errors raise LcbHashError (liblcb errno codes).  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (ALG_IDS, DIGEST_SIZE, F_DEVICE, GOST256, GOST512, MD5, SHA1, SHA224,
+                   SHA256, SHA384, SHA512, check, lib)
+
+__all__ = [
+    "hash_batch", "md5_get_digest_batch", "md5_hmac_get_digest_batch",
+    "sha1_get_digest_batch", "sha1_hmac_get_digest_batch", "sha2_get_digest_batch",
+    "sha2_hmac_get_digest_batch", "gost3411_2012_get_digest_batch",
+    "gost3411_2012_hmac_get_digest_batch", "gen_synthetic", "sha2_alg", "gost_alg",
+]
+
+
+def sha2_alg(bits):
+    """sha2_init's bits-or-bytes convention (sha2.h:217-241); None if invalid."""
+    return {224: SHA224, 28: SHA224, 256: SHA256, 32: SHA256,
+            384: SHA384, 48: SHA384, 512: SHA512, 64: SHA512}.get(int(bits))
+
+
+def gost_alg(bits):
+    """gost3411_2012_init (gost3411-2012.h:1715-1729): 256/32 -> 256, else 512."""
+    return GOST256 if int(bits) in (256, 32) else GOST512
+
+
+def _is_dev(t):
+    return isinstance(t, torch.Tensor) and t.is_cuda
+
+
+def _layout(count, offsets, lengths, stride, fixed_len, nbytes):
+    if count is None:
+        if lengths is not None:
+            count = int(lengths.shape[0])
+        elif offsets is not None:
+            count = int(offsets.shape[0])
+        elif stride:
+            count = nbytes // int(stride)
+        else:
+            raise ValueError("count is required for a fixed-length batch without stride")
+    if lengths is None and fixed_len is None:
+        fixed_len = int(stride or 0)
+    return int(count), int(stride or 0), int(fixed_len or 0)
+
+
+def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None,
+               fixed_len=None, key=None, out=None):
+    """Digest (or HMAC when `key` is given) of every message of a batch.
+
+    data     uint8 torch CUDA tensor (device mode) or numpy uint8 / bytes (host)
+    offsets  int64/uint64 per-message start offsets, or None (i * stride)
+    lengths  int32/uint32 per-message lengths, or None (fixed_len)
+    returns  packed digests, shape (count, D), same kind of memory as `data`
+    """
+    if isinstance(alg, str):
+        alg = ALG_IDS[alg]
+    if alg not in DIGEST_SIZE:
+        raise _lib.LcbHashError(22, "liblcb_hash_gpu: invalid argument (unknown alg)")
+    D = DIGEST_SIZE[alg]
+    kb = None if key is None else bytes(key)
+    kptr = ctypes.c_char_p(kb) if kb is not None else None
+    klen = len(kb) if kb is not None else 0
+    L = lib()
+    if _is_dev(data):
+        assert data.dtype == torch.uint8 and data.is_contiguous()
+        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
+        for t, dt in ((offsets, (torch.int64, torch.uint64)), (lengths, (torch.int32, torch.uint32))):
+            if t is not None:
+                assert _is_dev(t) and t.dtype in dt and t.is_contiguous() and t.device == data.device
+        if out is None:
+            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+        with torch.cuda.device(data.device):
+            stream = torch.cuda.current_stream(data.device).cuda_stream
+            check(L.lcb_hash_batch(alg, kptr, klen, data.data_ptr(),
+                                   offsets.data_ptr() if offsets is not None else None,
+                                   lengths.data_ptr() if lengths is not None else None,
+                                   count, stride, fixed_len, out.data_ptr(), F_DEVICE, stream))
+        return out
+    # host mode
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        data = np.frombuffer(bytes(data), dtype=np.uint8)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if data.size == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    if out is None:
+        out = np.empty((count, D), dtype=np.uint8)
+    check(L.lcb_hash_batch(alg, kptr, klen, data.ctypes.data,
+                           offsets.ctypes.data if offsets is not None else None,
+                           lengths.ctypes.data if lengths is not None else None,
+                           count, stride, fixed_len, out.ctypes.data, 0, None))
+    return out
+
+
+# ----------------------------------------------- reference-named wrappers
+def md5_get_digest_batch(data, **kw):
+    """Batch md5_get_digest (md5.h:396-402)."""
+    return hash_batch(MD5, data, **kw)
+
+
+def md5_hmac_get_digest_batch(key, data, **kw):
+    """Batch md5_hmac_get_digest (md5.h:419-425)."""
+    return hash_batch(MD5, data, key=key, **kw)
+
+
+def sha1_get_digest_batch(data, **kw):
+    """Batch sha1_get_digest (sha1.h:946-954)."""
+    return hash_batch(SHA1, data, **kw)
+
+
+def sha1_hmac_get_digest_batch(key, data, **kw):
+    """Batch sha1_hmac_get_digest (sha1.h:969-975)."""
+    return hash_batch(SHA1, data, key=key, **kw)
+
+
+def _sha2(bits):
+    alg = sha2_alg(bits)
+    if alg is None:  # sha2_init leaves an unknown size undefined; we refuse it
+        raise _lib.LcbHashError(22, "liblcb_hash_gpu: invalid argument (sha2 bits %r)" % (bits,))
+    return alg
+
+
+def sha2_get_digest_batch(bits, data, **kw):
+    """Batch sha2_get_digest (sha2.h:854-865); bits as sha2_init."""
+    return hash_batch(_sha2(bits), data, **kw)
+
+
+def sha2_hmac_get_digest_batch(bits, key, data, **kw):
+    """Batch sha2_hmac_get_digest (sha2.h:887-894)."""
+    return hash_batch(_sha2(bits), data, key=key, **kw)
+
+
+def gost3411_2012_get_digest_batch(bits, data, **kw):
+    """Batch gost3411_2012_get_digest (gost3411-2012.h:1962-1973)."""
+    return hash_batch(gost_alg(bits), data, **kw)
+
+
+def gost3411_2012_hmac_get_digest_batch(bits, key, data, **kw):
+    """Batch gost3411_2012_hmac_get_digest (gost3411-2012.h:1996-2004)."""
+    return hash_batch(gost_alg(bits), data, key=key, **kw)
+
+
+def gen_synthetic(seed, nbytes, start=0, device="cuda", out=None):
+    """Device tensor holding bytes [start, start+nbytes) of the synthetic stream
+    (u64 word k = mix64(seed ^ k), little-endian)."""
+    if out is None:
+        out = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+    with torch.cuda.device(out.device):
+        stream = torch.cuda.current_stream(out.device).cuda_stream
+        check(lib().lcb_hash_gen_synthetic(seed, start, out.data_ptr(), int(nbytes), stream))
+    return out[:int(nbytes)]

@@ -1,0 +1,135 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes access to the CPU checkers:
+  * Oracle  — oracle/liblcb_oracle.so, the C restatement (lcb_oracle.c);
+  * Ref     — oracle/_ref/libref_hash*.so, the reference's own headers
+              compiled from /root/reference (present only if built here).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liblcb_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_hash.so")
+REF_SIMD_SO = os.path.join(HERE, "_ref", "libref_hash_simd.so")
+DSIZE = {1: 16, 2: 20, 3: 28, 4: 32, 5: 48, 6: 64, 7: 32, 8: 64}
+SEED = 0x6C62636861736821
+
+_c = ctypes
+
+
+def build():
+    """Build the oracle (and _ref where /root/reference exists)."""
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def gen_stream(seed, nbytes, start=0):
+    """Bytes [start, start+nbytes) of the synthetic stream: u64 word k is
+    mix64(seed ^ k), little-endian."""
+    w0 = start // 8
+    nw = (start + nbytes + 7) // 8 - w0
+    k = np.arange(w0, w0 + nw, dtype=np.uint64)
+    z = (k ^ np.uint64(seed)) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    off = start - w0 * 8
+    return b[off:off + nbytes]
+
+
+class _Batch:
+    fn_batch = None
+
+    def batch(self, alg, data, offsets=None, lengths=None, count=None, stride=0,
+              fixed_len=0, key=None):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if count is None:
+            count = len(lengths) if lengths is not None else len(offsets)
+        out = np.zeros((count, DSIZE[alg]), dtype=np.uint8)
+        kb = bytes(key) if key is not None else None
+        rc = self.fn_batch(alg, kb, len(kb) if kb is not None else 0, data.ctypes.data,
+                           offsets.ctypes.data if offsets is not None else None,
+                           lengths.ctypes.data if lengths is not None else None,
+                           count, stride, fixed_len, out.ctypes.data)
+        assert rc == 0, rc
+        return out
+
+    def batch_fixed_mt(self, alg, data, count, stride, fixed_len, key=None, threads=8):
+        """Fixed-stride batch split into `threads` contiguous shards (ctypes
+        releases the GIL, so the shards run in parallel)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        out = np.zeros((count, DSIZE[alg]), dtype=np.uint8)
+        per = (count + threads - 1) // threads
+        kb = bytes(key) if key is not None else None
+
+        def work(t):
+            lo, hi = t * per, min(count, (t + 1) * per)
+            if lo < hi:
+                self.fn_batch(alg, kb, len(kb) if kb is not None else 0,
+                              data.ctypes.data + lo * stride, None, None, hi - lo, stride,
+                              fixed_len, out.ctypes.data + lo * DSIZE[alg])
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(work, range(threads)))
+        return out
+
+
+_ARGS = [_c.c_int, _c.c_char_p, _c.c_size_t, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+         _c.c_size_t, _c.c_uint64, _c.c_uint32, _c.c_void_p]
+
+
+class Oracle(_Batch):
+    """The C restatement."""
+
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            build()
+        self.lib = _c.CDLL(path)
+        self.lib.or_batch.argtypes = _ARGS
+        self.fn_batch = self.lib.or_batch
+        self.lib.or_init.argtypes = [_c.c_void_p, _c.c_int]
+        self.lib.or_update.argtypes = [_c.c_void_p, _c.c_char_p, _c.c_size_t]
+        self.lib.or_final.argtypes = [_c.c_void_p, _c.c_char_p]
+
+    def chunked(self, alg, msg, chunks):
+        """Streaming digest feeding `msg` in pieces of the given size."""
+        ctx = _c.create_string_buffer(512)
+        out = _c.create_string_buffer(64)
+        assert self.lib.or_init(ctx, alg) == 0
+        i = 0
+        while i < len(msg):
+            n = min(chunks, len(msg) - i)
+            self.lib.or_update(ctx, msg[i:i + n], n)
+            i += n
+        self.lib.or_final(ctx, out)
+        return out.raw[:DSIZE[alg]]
+
+
+class Ref(_Batch):
+    """The reference's own code (compiled from /root/reference into _ref/)."""
+
+    def __init__(self, path=REF_SO):
+        self.lib = _c.CDLL(path)
+        self.lib.ref_batch.argtypes = _ARGS
+        self.fn_batch = self.lib.ref_batch
+        self.lib.ref_gost_ax.argtypes = [_c.c_void_p]
+
+    @staticmethod
+    def available(path=REF_SO):
+        return os.path.exists(path)
+
+    def gost_ax(self):
+        t = np.zeros(2048, dtype=np.uint64)
+        self.lib.ref_gost_ax(t.ctypes.data)
+        return t

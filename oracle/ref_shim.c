@@ -1,0 +1,145 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Thin C wrapper that compiles the REFERENCE's own hash headers, where they
+ * lie under /root/reference/include (nothing is copied), into
+ * oracle/_ref/libref_hash*.so.  Used (a) to validate the oracle restatement
+ * and generate golden fixtures (tests/golden/make_golden.py) and (b) as the
+ * timed "reference CPU path" in bench.py's cpu_baseline leg.
+ *
+ * Build variants (oracle/Makefile):
+ *   libref_hash.so       generic, exactly as tests/hash/main.c:36 builds it
+ *                        (#undef __SSE2__): generic SHA-1 / GOST paths.
+ *   libref_hash_simd.so  REF_SIMD=1: SSE4.1/SSSE3/SHA-NI/AVX2 code paths of
+ *                        sha1.h / sha2.h / gost3411-2012.h enabled; the
+ *                        reference still picks them per ctx with cpuid.
+ */
+#include <sys/param.h>
+#include <sys/types.h>
+#include <inttypes.h>
+#include <stdio.h>
+
+#ifdef REF_SIMD
+#	include <immintrin.h>   /* sha1.h:91 / sha2.h:50 need it first */
+#else
+#	undef __SSE2__          /* tests/hash/main.c:36 */
+#endif
+
+#define MD5_SELF_TEST 1
+#define SHA1_SELF_TEST 1
+#define SHA2_SELF_TEST 1
+#define GOST3411_2012_SELF_TEST 1
+
+#include "crypto/hash/md5.h"
+#include "crypto/hash/sha1.h"
+#include "crypto/hash/sha2.h"
+#include "crypto/hash/gost3411-2012.h"
+
+enum { A_MD5 = 1, A_SHA1, A_SHA224, A_SHA256, A_SHA384, A_SHA512, A_GOST256, A_GOST512 };
+
+static size_t
+ref_bits(int alg) {
+	static const size_t b[9] = { 0, 0, 0, 224, 256, 384, 512, 256, 512 };
+	return (alg >= 1 && alg <= 8) ? b[alg] : 0;
+}
+
+/* tests/hash/main.c:53-82: first failing self test's code, else 0. */
+int
+ref_self_test(void) {
+	int e;
+	if ((e = md5_self_test())) return 100 + e;
+	if ((e = sha1_self_test())) return 200 + e;
+	if ((e = sha2_self_test())) return 300 + e;
+	if ((e = gost3411_2012_self_test())) return 400 + e;
+	return 0;
+}
+
+/* One digest through the reference's one-shot API. */
+static int
+ref_one(int alg, const uint8_t *d, size_t n, uint8_t *out) {
+	switch (alg) {
+	case A_MD5: md5_get_digest(d, n, out); return 0;
+	case A_SHA1: sha1_get_digest(d, n, out); return 0;
+	case A_SHA224: case A_SHA256: case A_SHA384: case A_SHA512:
+		sha2_get_digest(ref_bits(alg), d, n, out, NULL); return 0;
+	case A_GOST256: case A_GOST512:
+		gost3411_2012_get_digest(ref_bits(alg), d, n, out, NULL); return 0;
+	}
+	return -1;
+}
+
+static int
+ref_one_hmac(int alg, const uint8_t *k, size_t kl, const uint8_t *d, size_t n,
+    uint8_t *out) {
+	switch (alg) {
+	case A_MD5: md5_hmac_get_digest(k, kl, d, n, out); return 0;
+	case A_SHA1: sha1_hmac_get_digest(k, kl, d, n, out); return 0;
+	case A_SHA224: case A_SHA256: case A_SHA384: case A_SHA512:
+		sha2_hmac_get_digest(ref_bits(alg), k, kl, d, n, out, NULL); return 0;
+	case A_GOST256: case A_GOST512:
+		gost3411_2012_hmac_get_digest(ref_bits(alg), k, kl, d, n, out, NULL); return 0;
+	}
+	return -1;
+}
+
+static size_t
+ref_dsize(int alg) {
+	static const size_t ds[9] = { 0, 16, 20, 28, 32, 48, 64, 32, 64 };
+	return (alg >= 1 && alg <= 8) ? ds[alg] : 0;
+}
+
+/* Batch loop: message i at base + (offsets ? offsets[i] : i*stride), length
+ * (lengths ? lengths[i] : fixed_len); key != NULL selects HMAC. */
+int
+ref_batch(int alg, const uint8_t *key, size_t key_len, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lengths, size_t count,
+    uint64_t stride, uint32_t fixed_len, uint8_t *digests) {
+	size_t i, ds = ref_dsize(alg);
+
+	if (0 == ds)
+		return -1;
+	for (i = 0; i < count; i ++) {
+		const uint8_t *p = base + (offsets ? offsets[i] : (uint64_t)i * stride);
+		size_t n = (lengths ? lengths[i] : fixed_len);
+		if (key)
+			ref_one_hmac(alg, key, key_len, p, n, digests + i * ds);
+		else
+			ref_one(alg, p, n, digests + i * ds);
+	}
+	return 0;
+}
+
+/* Streaming with fixed-size update chunks (chunk 0 = whole message);
+ * exercises *_update buffering like gost3411-2012.h:2162-2230. */
+int
+ref_chunked(int alg, const uint8_t *d, size_t n, size_t chunk, uint8_t *out) {
+	size_t i, c;
+
+	if (0 == chunk)
+		chunk = (n ? n : 1);
+	switch (alg) {
+	case A_MD5: { md5_ctx_t x; md5_init(&x);
+		for (i = 0; i < n; i += c) { c = MIN(chunk, n - i); md5_update(&x, d + i, c); }
+		md5_final(&x, out); return 0; }
+	case A_SHA1: { sha1_ctx_t x; sha1_init(&x);
+		for (i = 0; i < n; i += c) { c = MIN(chunk, n - i); sha1_update(&x, d + i, c); }
+		sha1_final(&x, out); return 0; }
+	case A_SHA224: case A_SHA256: case A_SHA384: case A_SHA512: {
+		sha2_ctx_t x; sha2_init(ref_bits(alg), &x);
+		for (i = 0; i < n; i += c) { c = MIN(chunk, n - i); sha2_update(&x, d + i, c); }
+		sha2_final(&x, out); return 0; }
+	case A_GOST256: case A_GOST512: {
+		gost3411_2012_ctx_t x; gost3411_2012_init(ref_bits(alg), &x);
+		for (i = 0; i < n; i += c) { c = MIN(chunk, n - i); gost3411_2012_update(&x, d + i, c); }
+		gost3411_2012_final(&x, out); return 0; }
+	}
+	return -1;
+}
+
+/* GOST big-table export, so tests can pin the generated Ax tables
+ * (liblcb_amd) against gost3411-2012.h:184-882. */
+int
+ref_gost_ax(uint64_t *out /* 8*256 */) {
+	memcpy(out, gost3411_2012_Ax, sizeof(gost3411_2012_Ax));
+	return (int)sizeof(gost3411_2012_Ax);
+}

@@ -1,0 +1,66 @@
+"""Rebuild the inputs of a tests/golden/batches.json entry (data, layout, key).
+
+The fixtures hold seeds and layout rules, not bytes: the input is the
+synthetic stream of oracle.pyoracle.gen_stream (host) or
+liblcb_amd.gen_synthetic (device), which produce identical bytes.
+"""
+import hashlib
+
+import numpy as np
+
+SEED = 0x6C62636861736821
+M64 = (1 << 64) - 1
+
+
+def mixed_lengths(seed, count):
+    out = []
+    for i in range(count):
+        z = (seed + i + 0x9E3779B97F4A7C15) & M64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        z ^= z >> 31
+        out.append((64, 1024, 65536)[z % 3])
+    return out
+
+
+def layout(entry):
+    """-> dict(seed, nbytes, offsets|None, lengths|None, count, stride, fixed_len, key)."""
+    name = entry["name"]
+    key = bytes.fromhex(entry["key_hex"]) if "key_hex" in entry else None
+    if name.startswith("ragged_0_4159") or name == "mixed_512":
+        lens = (np.arange(4160, dtype=np.uint32) if name.startswith("ragged")
+                else np.array(mixed_lengths(SEED, 512), dtype=np.uint32))
+        offs = np.zeros(len(lens), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return dict(seed=SEED, nbytes=int(lens.sum()), offsets=offs, lengths=lens,
+                    count=len(lens), stride=0, fixed_len=0, key=key)
+    if name == "misaligned_2048":
+        lens = np.array(entry["lengths"], dtype=np.uint32)
+        offs = np.array(entry["offsets"], dtype=np.uint64)
+        return dict(seed=SEED ^ entry["seed_xor"], nbytes=int(offs[-1] + lens[-1]), offsets=offs,
+                    lengths=lens, count=len(lens), stride=0, fixed_len=0, key=key)
+    if name.startswith("big_"):
+        n = entry["fixed_len"]
+        return dict(seed=SEED, nbytes=n, offsets=None, lengths=None, count=1, stride=0,
+                    fixed_len=n, key=key)
+    # fixed-stride 1 KiB batches
+    c = entry["count"]
+    return dict(seed=SEED, nbytes=c * entry["stride"], offsets=None, lengths=None, count=c,
+                stride=entry["stride"], fixed_len=entry["fixed_len"], key=key)
+
+
+def dod(digests):
+    """SHA-256 over the packed digest array (fixture 'digest of digests')."""
+    return hashlib.sha256(np.ascontiguousarray(digests).tobytes()).hexdigest()
+
+
+def check_entry(entry, digests):
+    """Assert `digests` (count x D numpy) match every field the fixture keeps."""
+    d = np.ascontiguousarray(digests)
+    if "dod" in entry:
+        assert dod(d) == entry["dod"], (entry["name"], entry["alg"], entry.get("key"))
+    if "first" in entry:
+        n = len(entry["first"]) // 2
+        assert d.tobytes()[:n].hex() == entry["first"], (entry["name"], entry["alg"])
+    if "digest" in entry:
+        assert d.tobytes().hex() == entry["digest"], (entry["name"], entry["alg"])

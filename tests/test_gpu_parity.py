@@ -1,0 +1,213 @@
+"""Parity of the MI355X kernels (through the C-ABI) with the reference.
+
+Checkers: the reference's KAT tables (kat.json), digests the compiled
+reference produced (batches.json), and the oracle restatement (full digest
+arrays, same seeded inputs).  Bar: bit-exact.  Every test runs through
+liblcb_hash_gpu.so; nothing here computes a digest on the CPU except the
+oracle it compares against.
+"""
+import errno
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.pyoracle import gen_stream
+from tests.golden_util import check_entry, dod, layout
+
+pytestmark = pytest.mark.gpu
+
+ALG = {"md5": 1, "sha1": 2, "sha224": 3, "sha256": 4, "sha384": 5, "sha512": 6,
+       "gost256": 7, "gost512": 8}
+
+
+def dev(x, dtype=None):
+    return torch.as_tensor(np.ascontiguousarray(x), device="cuda") if dtype is None else \
+        torch.as_tensor(np.ascontiguousarray(x).astype(dtype), device="cuda")
+
+
+def run_entry(gpu, e, mode="device"):
+    L = layout(e)
+    alg = ALG[e["alg"]]
+    if mode == "device":
+        data = gpu.gen_synthetic(L["seed"], L["nbytes"])
+        offs = dev(L["offsets"], np.int64) if L["offsets"] is not None else None
+        lens = dev(L["lengths"], np.int32) if L["lengths"] is not None else None
+        d = gpu.hash_batch(alg, data, offsets=offs, lengths=lens, count=L["count"],
+                           stride=L["stride"], fixed_len=L["fixed_len"], key=L["key"])
+        torch.cuda.synchronize()
+        return d.cpu().numpy()
+    data = gen_stream(L["seed"], L["nbytes"])
+    return gpu.hash_batch(alg, data, offsets=L["offsets"], lengths=L["lengths"], count=L["count"],
+                          stride=L["stride"], fixed_len=L["fixed_len"], key=L["key"])
+
+
+def test_device_generator_matches_host(gpu):
+    for start, n in ((0, 4096), (3, 1000), (8, 77), (12345, 1 << 16)):
+        d = gpu.gen_synthetic(0x1234, n, start=start).cpu().numpy()
+        assert np.array_equal(d, gen_stream(0x1234, n, start)), (start, n)
+
+
+@pytest.mark.parametrize("mode", ["device", "host"])
+def test_kat(gpu, kat, mode):
+    """Every vector of the reference self tests (tests/hash/main.c path)."""
+    for c in kat:
+        alg = ALG[c["alg"]]
+        msg = bytes.fromhex(c["msg"]) * c.get("repeat", 1)
+        key = bytes.fromhex(c["key"]) if "key" in c else None
+        arr = np.frombuffer(msg, np.uint8) if msg else np.zeros(1, np.uint8)
+        if mode == "device":
+            d = gpu.hash_batch(alg, dev(arr), count=1, fixed_len=len(msg), key=key).cpu().numpy()
+        else:
+            d = gpu.hash_batch(alg, arr, count=1, fixed_len=len(msg), key=key)
+        assert d[0].tobytes().hex() == c["digest"], (c["alg"], len(msg), "key" in c)
+
+
+def test_kat_as_one_ragged_batch(gpu, kat):
+    """All KAT messages of one algorithm in ONE ragged batch (mixed lanes)."""
+    for name, alg in ALG.items():
+        cases = [c for c in kat if c["alg"] == name and "key" not in c]
+        msgs = [bytes.fromhex(c["msg"]) * c.get("repeat", 1) for c in cases]
+        lens = np.array([len(m) for m in msgs], np.uint32)
+        offs = np.zeros(len(msgs), np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(msgs) or b"\0", np.uint8)
+        d = gpu.hash_batch(alg, dev(blob), offsets=dev(offs, np.int64), lengths=dev(lens, np.int32))
+        d = d.cpu().numpy()
+        for i, c in enumerate(cases):
+            assert d[i].tobytes().hex() == c["digest"], (name, i)
+
+
+SMALL = ("ragged_0_4159", "misaligned_2048", "big_65536", "big_65537", "mixed_512",
+         "fixed1k_1024", "C2_64k_x_1k")
+
+
+def test_golden_batches_device(gpu, batches):
+    n = 0
+    for e in batches["batches"]:
+        if e["name"] in SMALL:
+            check_entry(e, run_entry(gpu, e))
+            n += 1
+    assert n >= 120
+
+
+def test_golden_batches_host(gpu, batches):
+    for e in batches["batches"]:
+        if e["name"] in ("ragged_0_4159", "misaligned_2048", "big_65537") and "key" not in e:
+            check_entry(e, run_entry(gpu, e, mode="host"))
+
+
+@pytest.mark.parametrize("alg", list(ALG))
+def test_c3_full_size(gpu, batches, alg):
+    """BASELINE config C3 (1M x 1 KiB, the bench workload): digest-of-digests
+    from the compiled reference."""
+    e = [x for x in batches["batches"] if x["name"] == "C3_1M_x_1k" and x["alg"] == alg][0]
+    check_entry(e, run_entry(gpu, e))
+
+
+def test_full_digests_vs_oracle(gpu, oracle):
+    """Full digest arrays (not hashes of them) against the oracle on a ragged,
+    misaligned batch with HMAC keys around the block boundary."""
+    rng = np.random.RandomState(3)
+    lens = rng.randint(0, 600, size=700).astype(np.uint32)
+    gaps = rng.randint(0, 9, size=700)
+    offs = np.zeros(700, np.uint64)
+    pos = 5
+    for i in range(700):
+        offs[i] = pos
+        pos += int(lens[i]) + int(gaps[i])
+    data = gen_stream(99, pos)
+    ddata = dev(data)
+    for alg in range(1, 9):
+        for key in (None, b"", b"secret", bytes(range(64)), bytes(range(65)), bytes(range(128)),
+                    bytes(range(129)), bytes(300)):
+            exp = oracle.batch(alg, data, offs, lens, key=key)
+            got = gpu.hash_batch(alg, ddata, offsets=dev(offs, np.int64), lengths=dev(lens, np.int32),
+                                 key=key).cpu().numpy()
+            assert np.array_equal(got, exp), (alg, None if key is None else len(key))
+
+
+def test_every_alignment_and_tail_length(gpu, oracle):
+    """Start offsets 0..15 x lengths 0..200: every tail/padding branch and every
+    load path (16-B aligned, 4-B aligned, byte-misaligned)."""
+    lens, offs = [], []
+    pos = 0
+    for a in range(16):
+        for n in range(0, 201):
+            pos = (pos + 15) // 16 * 16 + a
+            offs.append(pos)
+            lens.append(n)
+            pos += n
+    lens = np.array(lens, np.uint32)
+    offs = np.array(offs, np.uint64)
+    data = gen_stream(5, pos + 16)
+    for alg in range(1, 9):
+        exp = oracle.batch(alg, data, offs, lens)
+        got = gpu.hash_batch(alg, dev(data), offsets=dev(offs, np.int64), lengths=dev(lens, np.int32))
+        assert np.array_equal(got.cpu().numpy(), exp), alg
+
+
+def test_unaligned_digest_output(gpu, oracle):
+    data = gen_stream(1, 64 * 100)
+    for alg in (1, 2, 6, 7):
+        D = gpu.DIGEST_SIZE[alg]
+        out = torch.zeros(100 * D + 3, dtype=torch.uint8, device="cuda")
+        view = out[3:]
+        gpu.lib().lcb_hash_batch(alg, None, 0, dev(data).data_ptr(), None, None, 100, 64, 64,
+                                 view.data_ptr(), 1, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        exp = oracle.batch(alg, data, count=100, stride=64, fixed_len=64)
+        assert np.array_equal(view.cpu().numpy().reshape(100, D), exp)
+        assert out[:3].sum().item() == 0
+
+
+def test_reference_named_entry_points(gpu, oracle):
+    data = gen_stream(2, 1024 * 300)
+    d = dev(data)
+    kw = dict(count=300, stride=1024, fixed_len=1000)
+    for fn, alg in ((gpu.md5_get_digest_batch, 1), (gpu.sha1_get_digest_batch, 2)):
+        assert np.array_equal(fn(d, **kw).cpu().numpy(), oracle.batch(alg, data, **kw))
+    for bits, alg in ((224, 3), (28, 3), (256, 4), (32, 4), (384, 5), (48, 5), (512, 6), (64, 6)):
+        assert np.array_equal(gpu.sha2_get_digest_batch(bits, d, **kw).cpu().numpy(),
+                              oracle.batch(alg, data, **kw))
+        assert np.array_equal(gpu.sha2_hmac_get_digest_batch(bits, b"k", d, **kw).cpu().numpy(),
+                              oracle.batch(alg, data, key=b"k", **kw))
+    for bits, alg in ((256, 7), (32, 7), (512, 8), (64, 8), (1, 8), (0, 8)):
+        assert np.array_equal(gpu.gost3411_2012_get_digest_batch(bits, d, **kw).cpu().numpy(),
+                              oracle.batch(alg, data, **kw))
+    assert np.array_equal(gpu.md5_hmac_get_digest_batch(b"radius-secret", d, **kw).cpu().numpy(),
+                          oracle.batch(1, data, key=b"radius-secret", **kw))
+    assert np.array_equal(gpu.sha1_hmac_get_digest_batch(b"", d, **kw).cpu().numpy(),
+                          oracle.batch(2, data, key=b"", **kw))
+    assert np.array_equal(gpu.gost3411_2012_hmac_get_digest_batch(256, b"x" * 70, d, **kw).cpu().numpy(),
+                          oracle.batch(7, data, key=b"x" * 70, **kw))
+    with pytest.raises(gpu.LcbHashError) as ei:
+        gpu.sha2_get_digest_batch(100, d, **kw)
+    assert ei.value.errno == errno.EINVAL
+
+
+def test_empty_and_zero_count(gpu, oracle):
+    d = dev(np.zeros(16, np.uint8))
+    for alg in range(1, 9):
+        got = gpu.hash_batch(alg, d, count=5, stride=0, fixed_len=0).cpu().numpy()
+        exp = oracle.batch(alg, np.zeros(1, np.uint8), count=5, stride=0, fixed_len=0)
+        assert np.array_equal(got, exp)
+        assert gpu.hash_batch(alg, d, count=0, fixed_len=4).shape == (0, gpu.DIGEST_SIZE[alg])
+
+
+def test_properties_full_size(gpu):
+    """Size-independent properties at the bench size (1M x 1 KiB): identical
+    messages give identical digests; a one-byte change flips exactly that
+    message's digest; the host pipeline equals the device path."""
+    n = 1 << 20
+    data = gpu.gen_synthetic(7, n * 1024)
+    base = gpu.hash_batch(1, data, count=n, stride=1024, fixed_len=1024)
+    data[1024 * 12345 + 17] ^= 1
+    flip = gpu.hash_batch(1, data, count=n, stride=1024, fixed_len=1024)
+    diff = (base != flip).any(dim=1).nonzero().flatten().tolist()
+    assert diff == [12345]
+    same = torch.zeros(1024 * 64, dtype=torch.uint8, device="cuda")
+    z = gpu.hash_batch(4, same, count=64, stride=1024, fixed_len=1024)
+    assert (z == z[0]).all()
+    host = gpu.hash_batch(1, data[:1 << 26].cpu().numpy(), count=1 << 16, stride=1024, fixed_len=1024)
+    assert np.array_equal(host, flip[:1 << 16].cpu().numpy())
