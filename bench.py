@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident GiB/s hashed, 1M x 1 KiB buffers per MI355X.
+
+One step = one pass of the batch digest kernel over the rank's shard of
+1,048,576 x 1,024-byte buffers (BASELINE.json configs[2]; at --gpus 8 the 8
+shards form configs[4], 8M x 1 KiB).  Inputs are generated on the device by
+the synthetic-stream kernel before timing (no host traffic in the timed
+region).  Shards are independent (weak scaling, no data-path collective);
+the only collectives are the barrier and the max-over-ranks of the time.
+
+Extra fields on the JSON line:
+  roofline      dominant kernel vs HBM peak (algorithmic bytes / HIP-event
+                kernel time); traffic from a committed rocprofv3 PMC summary
+                (profiles/pmc_<alg>.json) when one exists for this workload
+  cpu_baseline  the reference's own include/crypto code (oracle/_ref, built
+                from /root/reference) timed on this host's cores, rank 0, N=1
+  per_alg       the same measurement for every algorithm (N=1)
+  e2e           host-memory path: pinned input -> H2D -> kernel -> D2H
+  verify        GPU digests of the timed workload vs the CPU reference run
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import liblcb_amd  # noqa: E402
+from liblcb_amd._lib import ALG_IDS, ALG_NAMES, DIGEST_SIZE, F_DEVICE, check, lib  # noqa: E402
+
+SEED = 0x6C62636861736821
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MSG_LEN = 1024
+MSGS_PER_GPU = 1 << 20
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--alg", default="md5", choices=sorted(ALG_IDS))
+    p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    p.add_argument("--no-extras", action="store_true", help="skip per_alg / e2e")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    return p.parse_args()
+
+
+def hash_launch(alg, data, digests, count, stream):
+    return lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), None, None, count, MSG_LEN,
+                                MSG_LEN, digests.data_ptr(), F_DEVICE, stream)
+
+
+def time_alg(alg, data, digests, count, steps, warmup, world):
+    """Returns (wall seconds for `steps` passes, max over ranks; mean kernel ms)."""
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    for _ in range(warmup):
+        check(hash_launch(alg, data, digests, count, sp))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        check(hash_launch(alg, data, digests, count, sp))
+        e.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    kms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    return t, kms
+
+
+def pmc_traffic(alg, count):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, corrected
+    as MI355X_MICROARCH.md prescribes (FETCH_SIZE reads 1/2 of a wide
+    coalesced stream on gfx950: doubled; WRITE_SIZE exact; both in KiB)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % ALG_NAMES[alg])
+    if not os.path.exists(path):
+        return None
+    try:
+        j = json.load(open(path))
+        if j.get("count") != count or j.get("msg_len") != MSG_LEN:
+            return None
+        return float(j["hbm_bytes_per_launch"])
+    except (ValueError, KeyError):
+        return None
+
+
+def cpu_baseline(alg, count, threads):
+    """The reference's include/crypto path (oracle/_ref, compiled from the
+    reference headers) on this host's cores, over the same 1M x 1 KiB bytes.
+    Falls back to reporting the oracle restatement (kind "port") only if the
+    reference build is absent."""
+    from oracle.pyoracle import REF_SIMD_SO, REF_SO, Oracle, Ref, gen_stream
+    data = gen_stream(SEED, count * MSG_LEN)
+    res = {}
+    for kind, path in (("reference", REF_SO), ("reference-simd", REF_SIMD_SO)):
+        if os.path.exists(path):
+            r = Ref(path)
+            r.batch_fixed_mt(alg, data[:MSG_LEN * 1024], 1024, MSG_LEN, MSG_LEN, threads=threads)
+            t0 = time.perf_counter()
+            d = r.batch_fixed_mt(alg, data, count, MSG_LEN, MSG_LEN, threads=threads)
+            t = time.perf_counter() - t0
+            res[kind] = (count * MSG_LEN / t / 2**30, t, d)
+    if not res:
+        o = Oracle()
+        t0 = time.perf_counter()
+        d = o.batch_fixed_mt(alg, data, count, MSG_LEN, MSG_LEN, threads=threads)
+        t = time.perf_counter() - t0
+        res["port"] = (count * MSG_LEN / t / 2**30, t, d)
+    best = max(res, key=lambda k: res[k][0])
+    return best, res
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    alg = ALG_IDS[a.alg]
+    count = a.count
+    D = DIGEST_SIZE[alg]
+
+    # Rank r hashes buffers [r*count, (r+1)*count) of the global synthetic batch.
+    data = liblcb_amd.gen_synthetic(SEED, count * MSG_LEN, start=rank * count * MSG_LEN)
+    digests = torch.empty((count, D), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+
+    t, kms = time_alg(alg, data, digests, count, a.steps, a.warmup, world)
+    total_bytes = world * count * MSG_LEN * a.steps
+    value = total_bytes / t / 2**30
+    alg_bytes = count * (MSG_LEN + D)      # read every message once + write its digest
+    achieved = alg_bytes / (kms * 1e-3) / 1e9
+    traffic = pmc_traffic(alg, count)
+    out = {
+        "metric": "device-resident GiB/s hashed, 1M x 1 KiB buffers per GPU",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(t / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if alg not in (5, 6, 7, 8) else "u64",
+        "data": "synthetic (device-generated splitmix64 stream, SURVEY.md 8d)",
+        "config": {"workload": "%s digest of %d x %d B buffers per GPU" % (a.alg, count, MSG_LEN),
+                   "alg": a.alg, "buffers_per_gpu": count, "buffer_bytes": MSG_LEN,
+                   "total_buffers": world * count, "parallelism": "shard%d" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kms, 4),
+                     "algorithmic_bytes_per_launch": alg_bytes},
+    }
+
+    if rank == 0 and world == 1 and not a.no_extras:
+        per = {}
+        for name, aid in sorted(ALG_IDS.items(), key=lambda x: x[1]):
+            dg = torch.empty((count, DIGEST_SIZE[aid]), dtype=torch.uint8, device="cuda")
+            tt, km = time_alg(aid, data, dg, count, max(3, a.steps // 4), 1, 1)
+            ab = count * (MSG_LEN + DIGEST_SIZE[aid])
+            per[name] = {"GiB_s": round(count * MSG_LEN * max(3, a.steps // 4) / tt / 2**30, 2),
+                         "kernel_ms": round(km, 4),
+                         "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            del dg
+        out["per_alg"] = per
+        # End-to-end host path on the same bytes: pinned host input -> H2D ->
+        # kernel -> D2H digests (lcb_hash_batch host mode, double-buffered).
+        host = data.cpu().pin_memory()
+        hn = host.numpy()
+        hd = np.empty((count, D), dtype=np.uint8)
+        liblcb_amd.hash_batch(alg, hn[:64 * MSG_LEN], count=64, stride=MSG_LEN, fixed_len=MSG_LEN)
+        t0 = time.perf_counter()
+        liblcb_amd.hash_batch(alg, hn, count=count, stride=MSG_LEN, fixed_len=MSG_LEN, out=hd)
+        te = time.perf_counter() - t0
+        out["e2e"] = {"GiB_s": round(count * MSG_LEN / te / 2**30, 3),
+                      "path": "pinned host buffer -> 64 MiB chunks, 2 streams -> D2H digests"}
+        torch.cuda.synchronize()
+        gpu_dig = digests.cpu().numpy()
+        out["verify"] = {"e2e_equals_device": bool(np.array_equal(hd, gpu_dig))}
+
+    if rank == 0 and world == 1 and not a.no_cpu:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        best, res = cpu_baseline(alg, count, threads)
+        gbs, tcpu, dcpu = res[best]
+        gpu_dig = digests.cpu().numpy()
+        out["cpu_baseline"] = {
+            "value": round(gbs, 3), "unit": "GiB/s", "cores": threads, "kind": "reference"
+            if best.startswith("reference") else "port",
+            "build": best, "sample": "the full workload: %d x %d B, %s, one contiguous shard per thread"
+            % (count, MSG_LEN, a.alg),
+            "all": {k: round(v[0], 3) for k, v in res.items()},
+            "seconds": round(tcpu, 3)}
+        out.setdefault("verify", {})["gpu_equals_cpu_reference"] = bool(np.array_equal(gpu_dig, dcpu))
+        out["verify"]["digest_of_digests"] = hashlib.sha256(gpu_dig.tobytes()).hexdigest()
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
