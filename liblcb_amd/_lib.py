@@ -15,7 +15,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblcb_hash_gpu.so")
+# LCB_HASH_GPU_LIB selects an alternative build (tuning experiments only).
+LIB_PATH = os.environ.get("LCB_HASH_GPU_LIB") or os.path.join(HERE, "liblcb_hash_gpu.so")
 
 MD5, SHA1, SHA224, SHA256, SHA384, SHA512, GOST256, GOST512 = range(1, 9)
 ALG_NAMES = {MD5: "md5", SHA1: "sha1", SHA224: "sha224", SHA256: "sha256",

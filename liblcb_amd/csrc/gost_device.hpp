@@ -126,14 +126,21 @@ __device__ __forceinline__ void gost_lps(uint64_t o[8], const uint64_t x[8], con
     for (int j = 0; j < 8; ++j) { lo[j] = (uint32_t)x[j]; hi[j] = (uint32_t)(x[j] >> 32); }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint64_t acc = 0;
+        uint64_t v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t src = (i < 4) ? lo[j] : hi[j];
             const uint32_t b = __builtin_amdgcn_ubfe(src, 8u * (i & 3), 8u);
-            acc ^= T[j * 256 + b];
+            v[j] = T[j * 256 + b];
         }
-        o[i] = acc;
+        // 8-way XOR as bitop3 xor3 on each half: 4 ops per half instead of 7.
+        uint32_t l = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]),
+                          xor3((uint32_t)v[3], (uint32_t)v[4], (uint32_t)v[5]),
+                          (uint32_t)v[6] ^ (uint32_t)v[7]);
+        uint32_t h = xor3(xor3((uint32_t)(v[0] >> 32), (uint32_t)(v[1] >> 32), (uint32_t)(v[2] >> 32)),
+                          xor3((uint32_t)(v[3] >> 32), (uint32_t)(v[4] >> 32), (uint32_t)(v[5] >> 32)),
+                          (uint32_t)(v[6] >> 32) ^ (uint32_t)(v[7] >> 32));
+        o[i] = ((uint64_t)h << 32) | l;
     }
 }
 

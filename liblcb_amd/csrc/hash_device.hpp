@@ -18,6 +18,32 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
+// Occupancy targets (waves per SIMD) per algorithm, used as the second
+// __launch_bounds__ argument; overridable at build time for tuning runs.
+#ifndef LCB_OCC_MD5
+#define LCB_OCC_MD5 8
+#endif
+#ifndef LCB_OCC_SHA1
+#define LCB_OCC_SHA1 8
+#endif
+#ifndef LCB_OCC_SHA256
+#define LCB_OCC_SHA256 4
+#endif
+#ifndef LCB_OCC_SHA512
+#define LCB_OCC_SHA512 4
+#endif
+#ifndef LCB_PREFETCH
+#define LCB_PREFETCH 0
+#endif
+#ifndef LCB_PAIR_SHA256
+#define LCB_PAIR_SHA256 0
+#endif
+#ifndef LCB_OCC_GOST
+#define LCB_OCC_GOST 2
+#endif
+
 namespace lcbgpu {
 
 // ------------------------------------------------------------ primitives
@@ -33,9 +59,36 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t n) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
     return __builtin_amdgcn_perm(0u, x, 0x00010203u);  // v_perm_b32
 }
+// Any 3-input boolean function in one VALU op (gfx950 v_bitop3_b32); the
+// immediate is the truth table over (a, b, c) = (0xf0, 0xcc, 0xaa).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return a ^ b ^ c;  // v_xor3_b32
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+__device__ __forceinline__ uint32_t ch3(uint32_t x, uint32_t y, uint32_t z) {   // (x & y) | (~x & z)
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0xca);
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t x, uint32_t y, uint32_t z) {  // majority
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0xe8);
+}
+// 64-bit values as explicit (lo, hi) halves so rotates are v_alignbit pairs.
+struct u64p {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ u64p mk64(uint64_t v) { return u64p{(uint32_t)v, (uint32_t)(v >> 32)}; }
+__device__ __forceinline__ uint64_t v64(u64p a) { return ((uint64_t)a.hi << 32) | a.lo; }
+template <int N>
+__device__ __forceinline__ u64p rotr64p(u64p x) {
+    if (N < 32) return u64p{__builtin_amdgcn_alignbit(x.hi, x.lo, N), __builtin_amdgcn_alignbit(x.lo, x.hi, N)};
+    return u64p{__builtin_amdgcn_alignbit(x.lo, x.hi, N - 32), __builtin_amdgcn_alignbit(x.hi, x.lo, N - 32)};
+}
+template <int N>  // N < 32
+__device__ __forceinline__ u64p shr64p(u64p x) {
+    return u64p{__builtin_amdgcn_alignbit(x.hi, x.lo, N), x.hi >> N};
+}
+__device__ __forceinline__ u64p xor3p(u64p a, u64p b, u64p c) {
+    return u64p{xor3(a.lo, b.lo, c.lo), xor3(a.hi, b.hi, c.hi)};
+}
+__device__ __forceinline__ u64p add64p(u64p a, u64p b) { return mk64(v64(a) + v64(b)); }
 
 // ------------------------------------------------------- block loading
 // Bytes [p, p+64) of a message that has at least 64 bytes left, as 16 raw LE
@@ -62,6 +115,28 @@ __device__ __forceinline__ void load_full64(const uint8_t* p, uint32_t w[16]) {
         for (int k = 0; k < 17; ++k) d[k] = q[k];
 #pragma unroll
         for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    }
+}
+
+// Bytes [p, p+128) of a message with >= 128 bytes left: one whole cache line
+// per lane when 16-B aligned (both halves requested together, so the line is
+// fetched from HBM once even when L2 is under pressure).
+__device__ __forceinline__ void load_full128(const uint8_t* p, uint32_t w0[16], uint32_t w1[16]) {
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+    if ((ip & 15u) == 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = q[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            w0[4 * k + 0] = v[k].x; w0[4 * k + 1] = v[k].y; w0[4 * k + 2] = v[k].z; w0[4 * k + 3] = v[k].w;
+            w1[4 * k + 0] = v[k + 4].x; w1[4 * k + 1] = v[k + 4].y; w1[4 * k + 2] = v[k + 4].z;
+            w1[4 * k + 3] = v[k + 4].w;
+        }
+    } else {
+        load_full64(p, w0);
+        load_full64(p + 64, w1);
     }
 }
 
@@ -94,7 +169,8 @@ __device__ __forceinline__ void put_byte(uint32_t w[16], uint32_t pos, uint32_t 
 // ================================================================== MD5
 // md5.h:137-229.  Round functions in their bitop3-friendly forms.
 struct Md5 {
-    static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16;
+    static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_MD5;
+    static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -103,10 +179,10 @@ struct Md5 {
     a = b + rotl32(a + (f) + (x) + (t), r)
     __device__ __forceinline__ void compress(const uint32_t* w) {
         uint32_t a = s[0], b = s[1], c = s[2], d = s[3];
-#define F1(b, c, d) (((c) ^ (d)) & (b)) ^ (d)
-#define F2(b, c, d) (((b) ^ (c)) & (d)) ^ (c)
-#define F3(b, c, d) ((b) ^ (c) ^ (d))
-#define F4(b, c, d) ((c) ^ ((b) | ~(d)))
+#define F1(b, c, d) ch3((b), (c), (d))
+#define F2(b, c, d) ch3((d), (b), (c))
+#define F3(b, c, d) xor3((b), (c), (d))
+#define F4(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x39)
         LCB_MD5_STEP(F1(b, c, d), a, b, c, d, w[0], 0xd76aa478u, 7);
         LCB_MD5_STEP(F1(a, b, c), d, a, b, c, w[1], 0xe8c7b756u, 12);
         LCB_MD5_STEP(F1(d, a, b), c, d, a, b, w[2], 0x242070dbu, 17);
@@ -196,7 +272,8 @@ struct Md5 {
 // ================================================================ SHA-1
 // sha1.h:220-292 with a 16-word rolling schedule.
 struct Sha1 {
-    static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16;
+    static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_SHA1;
+    static constexpr bool kPairLoad = true;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -213,13 +290,13 @@ struct Sha1 {
             if (i < 16) {
                 x = w[i];
             } else {
-                x = rotl32(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15]) ^ w[i & 15], 1);
+                x = rotl32(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15] ^ w[i & 15]), 1);
                 w[i & 15] = x;
             }
             uint32_t f, k;
-            if (i < 20) { f = ((c ^ d) & b) ^ d; k = 0x5a827999u; }
+            if (i < 20) { f = ch3(b, c, d); k = 0x5a827999u; }
             else if (i < 40) { f = xor3(b, c, d); k = 0x6ed9eba1u; }
-            else if (i < 60) { f = (b & c) | ((b | c) & d); k = 0x8f1bbcdcu; }
+            else if (i < 60) { f = maj3(b, c, d); k = 0x8f1bbcdcu; }
             else { f = xor3(b, c, d); k = 0xca62c1d6u; }
             const uint32_t t = rotl32(a, 5) + f + e + k + x;
             e = d; d = c; c = rotl32(b, 30); b = a; a = t;
@@ -252,7 +329,9 @@ __constant__ static const uint32_t kSha256K[64] = {
 
 template <bool k224>
 struct Sha256 {
-    static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16;
+    static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16,
+                         kOcc = LCB_OCC_SHA256;
+    static constexpr bool kPairLoad = LCB_PAIR_SHA256;  // VALU-bound: fewer live VGPRs
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -281,10 +360,10 @@ struct Sha256 {
                 w[i & 15] = x;
             }
             const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
-            const uint32_t ch = ((f ^ g) & e) ^ g;
+            const uint32_t ch = ch3(e, f, g);
             const uint32_t t1 = h + S1 + ch + kSha256K[i] + x;
             const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
-            const uint32_t mj = (a & b) | ((a | b) & c);
+            const uint32_t mj = maj3(a, b, c);
             h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
         }
         s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
@@ -302,7 +381,8 @@ struct Sha256 {
 // ============================================================ SHA-384/512
 // sha2.h:531-613; 64-bit words emulated on the 32-bit VALU (v_alignbit pairs,
 // v_add_co/addc or v_lshl_add_u64).  Raw words: 32 LE u32 per 128-B block.
-__constant__ static const uint64_t kSha512K[80] = {
+
+constexpr uint64_t kSha512Kc[80] = {
     0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
     0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
     0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
@@ -326,7 +406,9 @@ __constant__ static const uint64_t kSha512K[80] = {
 
 template <bool k384>
 struct Sha512 {
-    static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32;
+    static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32,
+                         kOcc = LCB_OCC_SHA512;
+    static constexpr bool kPairLoad = false;  // 128-B blocks already
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143
@@ -339,32 +421,46 @@ struct Sha512 {
             s[6] = 0x1f83d9abfb41bd6bull; s[7] = 0x5be0cd19137e2179ull;
         }
     }
-    __device__ __forceinline__ void compress(const uint32_t* raw) {
-        uint64_t w[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            w[i] = ((uint64_t)bswap32(raw[2 * i]) << 32) | bswap32(raw[2 * i + 1]);  // sha2.h:582
-        uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-#pragma unroll
-        for (int i = 0; i < 80; ++i) {
-            uint64_t x;
-            if (i < 16) {
-                x = w[i];
-            } else {
-                const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-                const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-                const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-                x = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-                w[i & 15] = x;
-            }
-            const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-            const uint64_t ch = ((f ^ g) & e) ^ g;
-            const uint64_t t1 = h + S1 + ch + kSha512K[i] + x;
-            const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-            const uint64_t mj = (a & b) | ((a | b) & c);
-            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    struct Vars {
+        u64p w[16];
+        u64p a, b, c, d, e, f, g, h;
+    };
+    // One round with a compile-time index (the 80 rounds are expanded by a
+    // fold expression, so every w[] index is static and w stays in VGPRs).
+    template <int i>
+    __device__ __forceinline__ static void round(Vars& v) {
+        u64p x;
+        if (i < 16) {
+            x = v.w[i];
+        } else {
+            const u64p w15 = v.w[(i - 15) & 15], w2 = v.w[(i - 2) & 15];
+            const u64p s0 = xor3p(rotr64p<1>(w15), rotr64p<8>(w15), shr64p<7>(w15));
+            const u64p s1 = xor3p(rotr64p<19>(w2), rotr64p<61>(w2), shr64p<6>(w2));
+            x = mk64(v64(v.w[i & 15]) + v64(s0) + v64(v.w[(i - 7) & 15]) + v64(s1));
+            v.w[i & 15] = x;
         }
-        s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+        const u64p S1 = xor3p(rotr64p<14>(v.e), rotr64p<18>(v.e), rotr64p<41>(v.e));
+        const u64p ch = u64p{ch3(v.e.lo, v.f.lo, v.g.lo), ch3(v.e.hi, v.f.hi, v.g.hi)};
+        const uint64_t t1 = v64(v.h) + v64(S1) + v64(ch) + kSha512Kc[i] + v64(x);
+        const u64p S0 = xor3p(rotr64p<28>(v.a), rotr64p<34>(v.a), rotr64p<39>(v.a));
+        const u64p mj = u64p{maj3(v.a.lo, v.b.lo, v.c.lo), maj3(v.a.hi, v.b.hi, v.c.hi)};
+        v.h = v.g; v.g = v.f; v.f = v.e; v.e = mk64(v64(v.d) + t1); v.d = v.c; v.c = v.b; v.b = v.a;
+        v.a = mk64(t1 + v64(S0) + v64(mj));
+    }
+    template <int... I>
+    __device__ __forceinline__ static void rounds(Vars& v, std::integer_sequence<int, I...>) {
+        (round<I>(v), ...);
+    }
+    __device__ __forceinline__ void compress(const uint32_t* raw) {
+        Vars v;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)  // BE u64 words (sha2.h:582)
+            v.w[i] = u64p{bswap32(raw[2 * i + 1]), bswap32(raw[2 * i])};
+        v.a = mk64(s[0]); v.b = mk64(s[1]); v.c = mk64(s[2]); v.d = mk64(s[3]);
+        v.e = mk64(s[4]); v.f = mk64(s[5]); v.g = mk64(s[6]); v.h = mk64(s[7]);
+        rounds(v, std::make_integer_sequence<int, 80>{});
+        s[0] += v64(v.a); s[1] += v64(v.b); s[2] += v64(v.c); s[3] += v64(v.d);
+        s[4] += v64(v.e); s[5] += v64(v.f); s[6] += v64(v.g); s[7] += v64(v.h);
     }
     // sha2.h:727-730: 128-bit BE bit length in bytes 112..127 (hi 64 bits =
     // bytes >> 61 for any length below 2^64 bytes).
@@ -436,7 +532,39 @@ __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t l
     uint32_t w[H::kWords];
     const uint64_t nfull = len / H::kBlock;
     const uint8_t* p = msg;
-    for (uint64_t b = 0; b < nfull; ++b, p += H::kBlock) {
+    uint64_t b = 0;
+    if (H::kPairLoad && LCB_PREFETCH) {
+        // Two blocks = one 128-B line per step, the next line's loads in
+        // flight while the current one is compressed (ping-pong buffers).
+        const uint64_t npair = nfull / 2;
+        if (npair > 0) {
+            uint32_t a0[16], a1[16], b0[16], b1[16];
+            load_full128(p, a0, a1);
+            uint64_t k = 0;
+            for (; k + 2 <= npair; k += 2, p += 256) {
+                load_full128(p + 128, b0, b1);
+                st.compress(a0);
+                st.compress(a1);
+                if (k + 2 < npair) load_full128(p + 256, a0, a1);
+                st.compress(b0);
+                st.compress(b1);
+            }
+            if (k < npair) {
+                st.compress(a0);
+                st.compress(a1);
+                p += 128;
+            }
+            b = 2 * npair;
+        }
+    } else if (H::kPairLoad) {  // two blocks = one 128-B line per iteration
+        uint32_t w1[16];
+        for (; b + 2 <= nfull; b += 2, p += 128) {
+            load_full128(p, w, w1);
+            st.compress(w);
+            st.compress(w1);
+        }
+    }
+    for (; b < nfull; ++b, p += H::kBlock) {
         load_block_full<H>(p, w);
         st.compress(w);
     }

@@ -22,7 +22,7 @@ __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint
 
 // ------------------------------------------------------------- MD family
 template <class H, bool kHmac>
-__global__ __launch_bounds__(256) void md_batch_kernel(KArgs a) {
+__global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
     uint64_t idx, len;
     const uint8_t* msg;
     if (!msg_at(a, idx, msg, len)) return;
@@ -78,7 +78,7 @@ __global__ void md_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t k
 
 // ------------------------------------------------------------------ GOST
 template <bool k256, bool kHmac>
-__global__ __launch_bounds__(256) void gost_batch_kernel(KArgs a) {
+__global__ __launch_bounds__(256, LCB_OCC_GOST) void gost_batch_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint64_t T[8 * 256];
     gost_stage_table(T);
     uint64_t idx, len;

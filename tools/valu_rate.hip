@@ -1,0 +1,107 @@
+// valu_rate.hip — measures issue throughput of the integer VALU instructions
+// the digest kernels are built from (cycles per wave64 instruction per SIMD).
+// Each thread runs 8 independent dependency chains of one instruction form in
+// inline asm; 256 CUs x 8 waves/SIMD.  Build: hipcc --offload-arch=gfx950 -O3
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#define REP8(X) X X X X X X X X
+#define CHAINS(OP) \
+    asm volatile(REP8(OP("%0") OP("%1") OP("%2") OP("%3") OP("%4") OP("%5") OP("%6") OP("%7")) \
+                 : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) \
+                 : "v"(k0), "v"(k1));
+
+#define OP_ADD(r) "v_add_u32 " r ", " r ", %8\n"
+#define OP_ADD3(r) "v_add3_u32 " r ", " r ", %8, %9\n"
+#define OP_ALIGNBIT(r) "v_alignbit_b32 " r ", " r ", %8, 7\n"
+#define OP_BITOP3(r) "v_bitop3_b32 " r ", " r ", %8, %9 bitop3:0x96\n"
+#define OP_XOR(r) "v_xor_b32 " r ", " r ", %8\n"
+#define OP_PERM(r) "v_perm_b32 " r ", " r ", %8, %9\n"
+#define OP_LSHLADD(r) "v_lshl_add_u32 " r ", " r ", 3, %8\n"
+#define OP_BFE(r) "v_bfe_u32 " r ", " r ", 8, 8\n"
+#define OP_XAD(r) "v_xad_u32 " r ", " r ", %8, %9\n"
+#define OP_FMA(r) "v_fma_f32 " r ", " r ", %8, %9\n"
+
+#define KERNEL(NAME, OP)                                                             \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {          \
+        unsigned r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, \
+                 r5 = r0 + 5, r6 = r0 + 6, r7 = r0 + 7;                              \
+        unsigned k0 = blockIdx.x | 1, k1 = 0x01010101u;                              \
+        for (int i = 0; i < iters; ++i) { CHAINS(OP) }                               \
+        out[blockIdx.x * 256 + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;  \
+    }
+
+KERNEL(k_add, OP_ADD)
+KERNEL(k_add3, OP_ADD3)
+KERNEL(k_alignbit, OP_ALIGNBIT)
+KERNEL(k_bitop3, OP_BITOP3)
+KERNEL(k_xor, OP_XOR)
+KERNEL(k_perm, OP_PERM)
+KERNEL(k_lshladd, OP_LSHLADD)
+KERNEL(k_bfe, OP_BFE)
+KERNEL(k_xad, OP_XAD)
+KERNEL(k_fma, OP_FMA)
+
+// 64-bit add forms used by SHA-512.
+__global__ __launch_bounds__(256) void k_lshl_add_u64(unsigned* out, int iters) {
+    unsigned long long a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned long long k = blockIdx.x | 1;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(REP8("v_lshl_add_u64 %0, %0, 0, %4\n v_lshl_add_u64 %1, %1, 0, %4\n"
+                          "v_lshl_add_u64 %2, %2, 0, %4\n v_lshl_add_u64 %3, %3, 0, %4\n"
+                          "v_lshl_add_u64 %0, %0, 0, %4\n v_lshl_add_u64 %1, %1, 0, %4\n"
+                          "v_lshl_add_u64 %2, %2, 0, %4\n v_lshl_add_u64 %3, %3, 0, %4\n")
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(k));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3);
+}
+__global__ __launch_bounds__(256) void k_addc_pair(unsigned* out, int iters) {
+    unsigned l0 = threadIdx.x, h0 = 1, l1 = l0 + 3, h1 = 2;
+    unsigned k = blockIdx.x | 1;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(REP8("v_add_co_u32 %0, vcc, %0, %4\n v_addc_co_u32 %1, vcc, %1, %4, vcc\n"
+                          "v_add_co_u32 %2, vcc, %2, %4\n v_addc_co_u32 %3, vcc, %3, %4, vcc\n"
+                          "v_add_co_u32 %0, vcc, %0, %4\n v_addc_co_u32 %1, vcc, %1, %4, vcc\n"
+                          "v_add_co_u32 %2, vcc, %2, %4\n v_addc_co_u32 %3, vcc, %3, %4, vcc\n")
+                     : "+v"(l0), "+v"(h0), "+v"(l1), "+v"(h1) : "v"(k) : "vcc");
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = l0 ^ h0 ^ l1 ^ h1;
+}
+
+typedef void (*kfn)(unsigned*, int);
+
+int main() {
+    unsigned* out;
+    hipMalloc(&out, 256 * 2048 * 8 * sizeof(unsigned));
+    struct { const char* name; kfn f; int ninstr; } ks[] = {
+        {"v_add_u32", k_add, 64}, {"v_add3_u32", k_add3, 64}, {"v_alignbit_b32", k_alignbit, 64},
+        {"v_bitop3_b32", k_bitop3, 64}, {"v_xor_b32", k_xor, 64}, {"v_perm_b32", k_perm, 64},
+        {"v_lshl_add_u32", k_lshladd, 64}, {"v_bfe_u32", k_bfe, 64}, {"v_xad_u32", k_xad, 64},
+        {"v_fma_f32", k_fma, 64}, {"v_lshl_add_u64", k_lshl_add_u64, 64},
+        {"v_add_co+addc (per instr)", k_addc_pair, 64}};
+    int dev;
+    hipGetDevice(&dev);
+    int clk_khz;
+    hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, dev);
+    const int blocks = 256 * 8;  // 8 blocks of 4 waves per CU = 8 waves/SIMD
+    const int iters = 4000;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (auto& k : ks) {
+        hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, 10);
+        hipDeviceSynchronize();
+        hipEventRecord(e0, 0);
+        hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, iters);
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        // wave-instructions per SIMD: blocks*4 waves / (256 CU * 4 SIMD) * iters * ninstr
+        double wi = (double)blocks * 4 / 1024.0 * iters * k.ninstr;
+        double cyc_at_peak = ms * 1e-3 * clk_khz * 1e3;
+        printf("%-28s %.3f ms  %.2f cycles/wave-instr/SIMD at %.0f MHz (lane-ops/s %.1f T)\n", k.name, ms,
+               cyc_at_peak / wi, clk_khz / 1e3, wi * 1024 * 64 / (ms * 1e-3) / 1e12);
+    }
+    return 0;
+}
