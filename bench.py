@@ -45,14 +45,31 @@ MSGS_PER_GPU = 1 << 20
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--alg", default="md5", choices=sorted(ALG_IDS))
     p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     p.add_argument("--no-extras", action="store_true", help="skip per_alg / e2e")
     p.add_argument("--cpu-threads", type=int, default=0)
     return p.parse_args()
+
+
+def shard_bounds(rank, world, per_gpu):
+    """Weak scaling: rank r owns buffers [r*per_gpu, (r+1)*per_gpu) of the
+    global batch, i.e. bytes starting at r*per_gpu*MSG_LEN of the stream."""
+    assert 0 <= rank < world
+    return rank * per_gpu, per_gpu
+
+
+def max_over_ranks(t, world):
+    """The job time is the slowest rank's (barrier-bracketed) time."""
+    if world == 1:
+        return t
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
 
 
 def hash_launch(alg, data, digests, count, stream):
@@ -83,11 +100,7 @@ def time_alg(alg, data, digests, count, steps, warmup, world):
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
     kms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
-    return t, kms
+    return max_over_ranks(t, world), kms
 
 
 def pmc_traffic(alg, count):
@@ -147,7 +160,8 @@ def main():
     D = DIGEST_SIZE[alg]
 
     # Rank r hashes buffers [r*count, (r+1)*count) of the global synthetic batch.
-    data = liblcb_amd.gen_synthetic(SEED, count * MSG_LEN, start=rank * count * MSG_LEN)
+    first, count = shard_bounds(rank, world, count)
+    data = liblcb_amd.gen_synthetic(SEED, count * MSG_LEN, start=first * MSG_LEN)
     digests = torch.empty((count, D), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
 
