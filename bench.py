@@ -145,6 +145,41 @@ def cpu_baseline(alg, count, threads):
     return best, res
 
 
+def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
+    """BASELINE configs[3]: 1M buffers, lengths {64 B, 1 KiB, 64 KiB} chosen by
+    mix64(seed + i) % 3, packed, device resident.  The library
+    buckets the ragged batch by length on the device (counted in the time)."""
+    from tests.golden_util import mixed_lengths
+    lens = np.array(mixed_lengths(SEED, count), dtype=np.uint32)
+    offs = np.zeros(count, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum())
+    data = liblcb_amd.gen_synthetic(SEED, total)
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    D = DIGEST_SIZE[alg]
+    dig = torch.empty((count, D), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        check(lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), do.data_ptr(), dl.data_ptr(), count,
+                                   0, 0, dig.data_ptr(), F_DEVICE, stream.cuda_stream))
+    for _ in range(warmup):
+        launch()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        launch()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    res = {"GiB_s": round(total / t / 2**30, 2), "ms_per_pass": round(t * 1e3, 3),
+           "total_GiB": round(total / 2**30, 2), "buffers": count,
+           "lengths": "{64, 1024, 65536}[mix64(seed+i) % 3]", "bucketed": True}
+    del data, dig
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,6 +239,7 @@ def main():
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
             del dg
         out["per_alg"] = per
+        out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
         # End-to-end host path on the same bytes: pinned host input -> H2D ->
         # kernel -> D2H digests (lcb_hash_batch host mode, double-buffered).
         host = data.cpu().pin_memory()

@@ -74,6 +74,22 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
     return 0;
 }
 
+// Launch the batch kernel, bucketing a large ragged batch by length first
+// (stream-ordered temporaries, no synchronisation).
+int launch_ordered(int alg, KArgs a, hipStream_t s) {
+    uint32_t* work = nullptr;
+    if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
+        const size_t bytes = (kLenClasses + a.count) * sizeof(uint32_t);
+        LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&work), bytes, s));
+        launch_bucketing(a.lengths, a.count, work, work + kLenClasses, s);
+        a.order = work + kLenClasses;
+    }
+    launch_batch(alg, a, s);
+    hipError_t e = hipGetLastError();
+    if (work) (void)hipFreeAsync(work, s);
+    return map_err(e);
+}
+
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                  uint32_t fixed_len, uint8_t* digests, hipStream_t s) {
@@ -88,11 +104,10 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
         if (rc) return rc;
         a.mid = mid;
     }
-    launch_batch(alg, a, s);
-    hipError_t e = hipGetLastError();
+    int rc = launch_ordered(alg, a, s);
     if (mid) (void)hipFreeAsync(mid, s);
     if (dkey) (void)hipFreeAsync(dkey, s);
-    return map_err(e);
+    return rc;
 }
 
 // ------------------------------------------------------------ host mode
@@ -225,8 +240,7 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
         KArgs a;
         a.data = S.d_data[b]; a.offsets = S.d_off[b]; a.lengths = S.d_len[b]; a.order = nullptr;
         a.count = n; a.stride = 0; a.fixed_len = 0; a.digests = S.d_dig[b]; a.mid = mid;
-        launch_batch(alg, a, s);
-        if (hipGetLastError() != hipSuccess ||
+        if (launch_ordered(alg, a, s) != 0 ||
             hipMemcpyAsync(S.h_dig[b], S.d_dig[b], n * D, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipEventRecord(S.done[b], s) != hipSuccess) {
             rc = EIO;

@@ -26,7 +26,14 @@ struct KeyBlock {
     uint32_t w[32];
 };
 
+// Length classes for ragged-batch bucketing (see lcb_kernels.hip).
+constexpr int kLenClasses = 128;
+// Ragged batches at least this large are bucketed by length first.
+constexpr uint64_t kBucketMinCount = 4096;
+
 void launch_batch(int alg, const KArgs& a, hipStream_t s);
+void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, uint32_t* order,
+                      hipStream_t s);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
                       uint32_t* mid, hipStream_t s);
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);

@@ -175,6 +175,78 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t seed, uint64_t start,
     }
 }
 
+// ---------------------------------------------------- length bucketing
+// Ragged batches: lanes of one wavefront run until the longest lane's message
+// is done, so a random mix of 64 B and 64 KiB messages would make almost
+// every wave as slow as a 64 KiB one.  These kernels compute a permutation
+// `order` that groups messages by block-count class, longest class first
+// (a counting sort; order inside a class is arbitrary and does not affect
+// any digest, which is always written at the message's own index).
+//   class(len) = nb for nb = len/64 + 1 < 64, else 58 + floor(log2(nb))
+// i.e. exact block counts up to 4 KiB, power-of-two bins above.
+__device__ __forceinline__ uint32_t len_class(uint64_t len) {
+    const uint64_t nb = (len >> 6) + 1;
+    if (nb < 64) return (uint32_t)nb;
+    return 58u + (63u - (uint32_t)__clzll((long long)nb));
+}
+
+__global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t* lengths, uint64_t count,
+                                                          uint32_t* hist) {
+    __shared__ uint32_t h[kLenClasses];
+    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x) h[c] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[len_class(lengths[i])], 1u);
+    __syncthreads();
+    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x)
+        if (h[c]) atomicAdd(&hist[c], h[c]);
+}
+
+// Exclusive prefix over classes in DESCENDING class order -> start cursor.
+__global__ void bucket_scan_kernel(uint32_t* hist_to_cursor) {
+    if (threadIdx.x != 0) return;
+    uint32_t run = 0;
+    for (int c = kLenClasses - 1; c >= 0; --c) {
+        const uint32_t n = hist_to_cursor[c];
+        hist_to_cursor[c] = run;
+        run += n;
+    }
+}
+
+// Each block reserves a contiguous range per class with one global atomic,
+// then scatters its indices (LDS atomics give the in-block rank).
+__global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t* lengths, uint64_t count,
+                                                             uint32_t* cursor, uint32_t* order) {
+    __shared__ uint32_t h[kLenClasses];
+    __shared__ uint32_t base[kLenClasses];
+    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x) h[c] = 0;
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t c = 0, r = 0;
+    if (i < count) {
+        c = len_class(lengths[i]);
+        r = atomicAdd(&h[c], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kLenClasses; k += blockDim.x)
+        base[k] = h[k] ? atomicAdd(&cursor[k], h[k]) : 0u;
+    __syncthreads();
+    if (i < count) order[base[c] + r] = (uint32_t)i;
+}
+
+void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, uint32_t* order,
+                      hipStream_t s) {
+    // work: kLenClasses uint32 (zeroed here); order: count uint32.
+    (void)hipMemsetAsync(work, 0, kLenClasses * sizeof(uint32_t), s);
+    uint64_t hb = (count + 255) / 256;
+    if (hb > 2048) hb = 2048;
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)hb), dim3(256), 0, s, lengths, count, work);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(64), 0, s, work);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s,
+                       lengths, count, work, order);
+}
+
 // ------------------------------------------------------------- launchers
 static inline dim3 grid_for(uint64_t count) { return dim3((unsigned)((count + 255) / 256)); }
 

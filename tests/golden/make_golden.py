@@ -295,6 +295,21 @@ def build_batches(ref, full):
         B.append(dict(name="mixed_512", alg=name, layout="packed", lengths="mix64(seed+i)%3",
                       count=512, dod=dod(d)))
 
+    # 4b) larger mixed batch: above the bucketing threshold (4096) of the GPU
+    #     path, so the length-bucketed ordering is exercised at C4's mix.
+    lens = np.array(mixed_lengths(SEED ^ 0xC4, 16384), dtype=np.uint32)
+    offs = np.zeros(16384, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    data = gen_stream(SEED ^ 0xC4, int(lens.sum()))
+    for name, alg in ALGS.items():
+        d = ref.batch(alg, data, offs, lens, 16384)
+        B.append(dict(name="mixed_16384", alg=name, layout="packed", lengths="mix64(seed^0xc4+i)%3",
+                      seed_xor=0xC4, count=16384, dod=dod(d)))
+        if name in ("md5", "sha256"):
+            dk = ref.batch(alg, data, offs, lens, 16384, key=HMAC_KEYS["k65"])
+            B.append(dict(name="mixed_16384", alg=name, layout="packed", seed_xor=0xC4,
+                          count=16384, key="k65", key_hex=HMAC_KEYS["k65"].hex(), dod=dod(dk)))
+
     # 5) fixed-stride 1 KiB batches: 1024 (full digests kept for MD5), C2 64K, C3 1M.
     sizes = [(1024, "fixed1k_1024"), (65536, "C2_64k_x_1k")]
     if full:

@@ -34,6 +34,13 @@ def layout(entry):
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
         return dict(seed=SEED, nbytes=int(lens.sum()), offsets=offs, lengths=lens,
                     count=len(lens), stride=0, fixed_len=0, key=key)
+    if name == "mixed_16384":
+        seed = SEED ^ entry["seed_xor"]
+        lens = np.array(mixed_lengths(seed, entry["count"]), dtype=np.uint32)
+        offs = np.zeros(len(lens), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return dict(seed=seed, nbytes=int(lens.sum()), offsets=offs, lengths=lens,
+                    count=len(lens), stride=0, fixed_len=0, key=key)
     if name == "misaligned_2048":
         lens = np.array(entry["lengths"], dtype=np.uint32)
         offs = np.array(entry["offsets"], dtype=np.uint64)

@@ -79,7 +79,7 @@ def test_kat_as_one_ragged_batch(gpu, kat):
 
 
 SMALL = ("ragged_0_4159", "misaligned_2048", "big_65536", "big_65537", "mixed_512",
-         "fixed1k_1024", "C2_64k_x_1k")
+         "mixed_16384", "fixed1k_1024", "C2_64k_x_1k")
 
 
 def test_golden_batches_device(gpu, batches):
@@ -93,7 +93,7 @@ def test_golden_batches_device(gpu, batches):
 
 def test_golden_batches_host(gpu, batches):
     for e in batches["batches"]:
-        if e["name"] in ("ragged_0_4159", "misaligned_2048", "big_65537") and "key" not in e:
+        if e["name"] in ("ragged_0_4159", "misaligned_2048", "big_65537", "mixed_16384") and "key" not in e:
             check_entry(e, run_entry(gpu, e, mode="host"))
 
 
@@ -211,3 +211,21 @@ def test_properties_full_size(gpu):
     assert (z == z[0]).all()
     host = gpu.hash_batch(1, data[:1 << 26].cpu().numpy(), count=1 << 16, stride=1024, fixed_len=1024)
     assert np.array_equal(host, flip[:1 << 16].cpu().numpy())
+
+
+def test_bucketed_equals_unbucketed(gpu, oracle):
+    """A ragged batch above the bucketing threshold (length-sorted lanes) gives
+    the same digests, in input order, as the same messages hashed in small
+    (unbucketed) batches."""
+    from tests.golden_util import mixed_lengths
+    n = 12000
+    lens = np.array(mixed_lengths(17, n), np.uint32) // np.array([1, 3, 7], np.uint32)[np.arange(n) % 3]
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    data = gpu.gen_synthetic(17, int(lens.sum()))
+    dl, do = dev(lens, np.int32), dev(offs, np.int64)
+    for alg in (1, 4, 7):
+        whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        parts = [gpu.hash_batch(alg, data, offsets=do[i:i + 1000], lengths=dl[i:i + 1000]).cpu().numpy()
+                 for i in range(0, n, 1000)]
+        assert np.array_equal(whole, np.concatenate(parts)), alg
