@@ -46,7 +46,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--alg", default="md5", choices=sorted(ALG_IDS))
     p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")

@@ -34,6 +34,13 @@
 #ifndef LCB_OCC_SHA512
 #define LCB_OCC_SHA512 4
 #endif
+// LDS-DMA staged fixed-stride kernel (lcb_kernels.hip): parity-green but
+// measured performance-neutral vs direct 128-B line loads on MI355X (MD5
+// 0.21 vs 0.20-0.21 ms per 1 GiB, both ~90% of the 5.9 TB/s streaming read
+// rate of tools/loadpat.hip) while capping occupancy at 5 waves/SIMD; off.
+#ifndef LCB_FIXED_LDS
+#define LCB_FIXED_LDS 0
+#endif
 #ifndef LCB_PREFETCH
 #define LCB_PREFETCH 0
 #endif
