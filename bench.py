@@ -240,17 +240,23 @@ def main():
             del dg
         out["per_alg"] = per
         out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
-        # End-to-end host path on the same bytes: pinned host input -> H2D ->
-        # kernel -> D2H digests (lcb_hash_batch host mode, double-buffered).
+        # End-to-end host path on the same bytes (lcb_hash_batch host mode):
+        # pinned input is DMA'd straight from the caller's buffer, pageable
+        # input is gathered into pinned staging first; 64 MiB chunks on two
+        # streams, H2D -> kernel -> D2H digests.
         host = data.cpu().pin_memory()
-        hn = host.numpy()
         hd = np.empty((count, D), dtype=np.uint8)
-        liblcb_amd.hash_batch(alg, hn[:64 * MSG_LEN], count=64, stride=MSG_LEN, fixed_len=MSG_LEN)
-        t0 = time.perf_counter()
-        liblcb_amd.hash_batch(alg, hn, count=count, stride=MSG_LEN, fixed_len=MSG_LEN, out=hd)
-        te = time.perf_counter() - t0
-        out["e2e"] = {"GiB_s": round(count * MSG_LEN / te / 2**30, 3),
-                      "path": "pinned host buffer -> 64 MiB chunks, 2 streams -> D2H digests"}
+        e2e = {}
+        for kind, arr in (("pinned", host.numpy()), ("pageable", np.array(host.numpy()))):
+            liblcb_amd.hash_batch(alg, arr[:64 * MSG_LEN], count=64, stride=MSG_LEN, fixed_len=MSG_LEN)
+            best = 1e9
+            for _ in range(3):
+                t0 = time.perf_counter()
+                liblcb_amd.hash_batch(alg, arr, count=count, stride=MSG_LEN, fixed_len=MSG_LEN, out=hd)
+                best = min(best, time.perf_counter() - t0)
+            e2e[kind + "_GiB_s"] = round(count * MSG_LEN / best / 2**30, 3)
+        e2e["path"] = "host buffer -> 64 MiB chunks, 2 streams, H2D -> kernel -> D2H digests"
+        out["e2e"] = e2e
         torch.cuda.synchronize()
         gpu_dig = digests.cpu().numpy()
         out["verify"] = {"e2e_equals_device": bool(np.array_equal(hd, gpu_dig))}

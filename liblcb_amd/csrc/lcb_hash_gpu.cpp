@@ -2,9 +2,9 @@
 //
 // Device mode enqueues on the caller's stream and never synchronises (except
 // to stage a long HMAC key, see hmac_setup).  Host mode runs a double-buffered
-// pipeline on two private streams: pinned staging -> hipMemcpyAsync H2D ->
-// kernel -> hipMemcpyAsync D2H, chunk c+1's upload overlapping chunk c's
-// kernel.  Every HIP failure maps to an errno code; nothing falls back to the
+// pipeline on two private streams: H2D -> kernel -> D2H per chunk, chunk c+1's
+// upload overlapping chunk c's kernel; page-locked input is DMA'd directly,
+// pageable input is gathered into pinned staging by up to 8 host threads.  Every HIP failure maps to an errno code; nothing falls back to the
 // CPU.
 #include <errno.h>
 #include <stdint.h>
@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -178,25 +179,63 @@ thread_local Stage g_stage;
 constexpr size_t kChunkBytes = 64ull << 20;   // 64 MiB per in-flight chunk
 constexpr size_t kChunkMsgs = 1u << 18;       // 256 K messages per chunk
 
+// True when `p` is page-locked host memory the DMA engines can read directly
+// (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory()).
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+// memcpy of many (dst, src, n) pieces, split over up to 8 host threads when
+// the chunk is large (the single-thread staging copy was the host-path bound).
+struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
+    const size_t nt = bytes >= (8u << 20) ? std::min<size_t>(8, pieces.size()) : 1;
+    if (nt <= 1) {
+        for (const Piece& p : pieces) memcpy(p.dst, p.src, p.n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (pieces.size() + nt - 1) / nt;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t lo = t * per, hi = std::min(pieces.size(), lo + per);
+        if (lo >= hi) break;
+        th.emplace_back([&pieces, lo, hi] {
+            for (size_t k = lo; k < hi; ++k) memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                uint32_t fixed_len, uint8_t* digests) {
     int dev = 0;
     LCB_TRY(hipGetDevice(&dev));
     const size_t D = dsize(alg);
+    const bool fixed = (offsets == nullptr && lengths == nullptr);
     auto off_of = [&](size_t i) -> uint64_t { return offsets ? offsets[i] : (uint64_t)i * stride; };
     auto len_of = [&](size_t i) -> uint64_t { return lengths ? lengths[i] : fixed_len; };
 
     // Largest single message decides the minimum buffer.
-    uint64_t maxlen = 0;
+    uint64_t maxlen = fixed_len;
     if (lengths) {
+        maxlen = 0;
         for (size_t i = 0; i < count; ++i) maxlen = std::max<uint64_t>(maxlen, lengths[i]);
-    } else {
-        maxlen = fixed_len;
     }
     int rc = g_stage.ensure(dev, std::max<size_t>(kChunkBytes, maxlen), kChunkMsgs);
     if (rc) return rc;
     Stage& S = g_stage;
+    const bool src_pinned = is_pinned(data);
+    const bool dig_pinned = is_pinned(digests);
 
     uint32_t* mid = nullptr;
     uint8_t* dkey = nullptr;
@@ -209,39 +248,80 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     auto drain = [&](int b) -> int {
         if (!S.busy[b]) return 0;
         LCB_TRY(hipEventSynchronize(S.done[b]));
-        memcpy(digests + S.pend_first[b] * D, S.h_dig[b], S.pend_n[b] * D);
+        if (!dig_pinned) memcpy(digests + S.pend_first[b] * D, S.h_dig[b], S.pend_n[b] * D);
         S.busy[b] = false;
         return 0;
     };
 
+    std::vector<Piece> pieces;
     size_t i = 0;
     int b = 0;
     while (i < count) {
         if ((rc = drain(b))) break;
-        // Gather a chunk of messages [i, j) whose bytes fit the staging buffer.
-        size_t j = i, bytes = 0;
-        while (j < count && j - i < S.mcap) {
-            const uint64_t n = len_of(j);
-            if (bytes + n > S.cap && j > i) break;
-            memcpy(S.h_data[b] + bytes, data + off_of(j), n);
-            S.h_off[b][j - i] = bytes;
-            S.h_len[b][j - i] = (uint32_t)n;
-            bytes += n;
-            ++j;
+        hipStream_t s = S.st[b];
+        // Choose messages [i, j): their bytes must fit one staging buffer.
+        size_t j = i;
+        uint64_t base = 0, span = 0, total = 0;
+        if (fixed) {
+            const size_t per = stride ? std::max<size_t>(1, (S.cap - fixed_len) / stride + 1) : S.mcap;
+            j = std::min(count, i + std::min(per, S.mcap));
+            base = (uint64_t)i * stride;
+            span = (uint64_t)(j - i - 1) * stride + fixed_len;
+            total = (uint64_t)(j - i) * fixed_len;
+        } else {
+            uint64_t lo = UINT64_MAX, hi = 0;
+            while (j < count && j - i < S.mcap) {
+                const uint64_t o = off_of(j), n = len_of(j);
+                const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, o + n);
+                if (j > i && (nhi - nlo > S.cap || total + n > S.cap)) break;
+                lo = nlo; hi = nhi; total += n;
+                ++j;
+            }
+            base = lo;
+            span = hi - lo;
         }
         const size_t n = j - i;
-        hipStream_t s = S.st[b];
-        if (hipMemcpyAsync(S.d_data[b], S.h_data[b], bytes ? bytes : 1, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(S.d_off[b], S.h_off[b], n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(S.d_len[b], S.h_len[b], n * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
-            rc = EIO;
-            break;
-        }
+        // Direct DMA from pinned input when the chunk's bytes are dense enough;
+        // otherwise gather the messages into pinned staging first.
+        const bool direct = src_pinned && span <= S.cap && (fixed || span <= 2 * total + 4096);
         KArgs a;
-        a.data = S.d_data[b]; a.offsets = S.d_off[b]; a.lengths = S.d_len[b]; a.order = nullptr;
-        a.count = n; a.stride = 0; a.fixed_len = 0; a.digests = S.d_dig[b]; a.mid = mid;
-        if (launch_ordered(alg, a, s) != 0 ||
-            hipMemcpyAsync(S.h_dig[b], S.d_dig[b], n * D, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        a.order = nullptr; a.count = n; a.digests = S.d_dig[b]; a.mid = mid;
+        bool ok = true;
+        if (direct) {
+            ok = hipMemcpyAsync(S.d_data[b], data + base, span ? span : 1, hipMemcpyHostToDevice, s) == hipSuccess;
+            if (fixed) {
+                a.data = S.d_data[b]; a.offsets = nullptr; a.lengths = nullptr;
+                a.stride = stride; a.fixed_len = fixed_len;
+            } else {
+                for (size_t k = 0; k < n; ++k) {
+                    S.h_off[b][k] = off_of(i + k) - base;
+                    S.h_len[b][k] = (uint32_t)len_of(i + k);
+                }
+                a.data = S.d_data[b]; a.offsets = S.d_off[b]; a.lengths = S.d_len[b];
+                a.stride = 0; a.fixed_len = 0;
+            }
+        } else {
+            pieces.clear();
+            uint64_t pos = 0;
+            for (size_t k = 0; k < n; ++k) {
+                const uint64_t ln = len_of(i + k);
+                pieces.push_back(Piece{S.h_data[b] + pos, data + off_of(i + k), (size_t)ln});
+                S.h_off[b][k] = pos;
+                S.h_len[b][k] = (uint32_t)ln;
+                pos += ln;
+            }
+            parallel_copy(pieces, pos);
+            ok = hipMemcpyAsync(S.d_data[b], S.h_data[b], pos ? pos : 1, hipMemcpyHostToDevice, s) == hipSuccess;
+            a.data = S.d_data[b]; a.offsets = S.d_off[b]; a.lengths = S.d_len[b];
+            a.stride = 0; a.fixed_len = 0;
+        }
+        if (ok && a.offsets) {
+            ok = hipMemcpyAsync(S.d_off[b], S.h_off[b], n * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+                 hipMemcpyAsync(S.d_len[b], S.h_len[b], n * 4, hipMemcpyHostToDevice, s) == hipSuccess;
+        }
+        if (!ok || launch_ordered(alg, a, s) != 0 ||
+            hipMemcpyAsync(dig_pinned ? digests + i * D : S.h_dig[b], S.d_dig[b], n * D,
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipEventRecord(S.done[b], s) != hipSuccess) {
             rc = EIO;
             break;

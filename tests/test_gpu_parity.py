@@ -229,3 +229,20 @@ def test_bucketed_equals_unbucketed(gpu, oracle):
         parts = [gpu.hash_batch(alg, data, offsets=do[i:i + 1000], lengths=dl[i:i + 1000]).cpu().numpy()
                  for i in range(0, n, 1000)]
         assert np.array_equal(whole, np.concatenate(parts)), alg
+
+
+def test_host_mode_pinned_direct_dma(gpu, batches):
+    """Host mode from page-locked input (direct DMA, rebased offsets for ragged
+    chunks) and from pageable input (parallel gather), multi-chunk sizes."""
+    for e in batches["batches"]:
+        if e["name"] not in ("ragged_0_4159", "mixed_16384", "C2_64k_x_1k", "misaligned_2048"):
+            continue
+        if "key" in e and e["name"] != "mixed_16384":
+            continue
+        L = layout(e)
+        host = gen_stream(L["seed"], L["nbytes"])
+        pinned = torch.empty(max(len(host), 1), dtype=torch.uint8).pin_memory()
+        pinned.numpy()[:len(host)] = host
+        d = gpu.hash_batch(ALG[e["alg"]], pinned.numpy(), offsets=L["offsets"], lengths=L["lengths"],
+                           count=L["count"], stride=L["stride"], fixed_len=L["fixed_len"], key=L["key"])
+        check_entry(e, d)
