@@ -21,6 +21,14 @@
 #define OP_BFE(r) "v_bfe_u32 " r ", " r ", 8, 8\n"
 #define OP_XAD(r) "v_xad_u32 " r ", " r ", %8, %9\n"
 #define OP_FMA(r) "v_fma_f32 " r ", " r ", %8, %9\n"
+#define OP_SHL(r) "v_lshlrev_b32 " r ", 3, " r "\n"
+#define OP_SHR(r) "v_lshrrev_b32 " r ", 3, " r "\n"
+#define OP_LSHLOR(r) "v_lshl_or_b32 " r ", " r ", 3, %8\n"
+#define OP_ALIGNBYTE(r) "v_alignbyte_b32 " r ", " r ", %8, 1\n"
+#define OP_MOV(r) "v_mov_b32 " r ", " r "\n"
+#define OP_BFI(r) "v_bfi_b32 " r ", " r ", %8, %9\n"
+#define OP_OR3(r) "v_or3_b32 " r ", " r ", %8, %9\n"
+#define OP_CNDMASK(r) "v_cndmask_b32 " r ", " r ", %8, vcc\n"
 
 #define KERNEL(NAME, OP)                                                             \
     __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {          \
@@ -41,6 +49,37 @@ KERNEL(k_lshladd, OP_LSHLADD)
 KERNEL(k_bfe, OP_BFE)
 KERNEL(k_xad, OP_XAD)
 KERNEL(k_fma, OP_FMA)
+KERNEL(k_shl, OP_SHL)
+KERNEL(k_shr, OP_SHR)
+KERNEL(k_lshlor, OP_LSHLOR)
+KERNEL(k_alignbyte, OP_ALIGNBYTE)
+KERNEL(k_mov, OP_MOV)
+KERNEL(k_bfi, OP_BFI)
+KERNEL(k_or3, OP_OR3)
+
+// 64-bit shifts and packed moves (rotate-by-64-bit-shift candidates).
+__global__ __launch_bounds__(256) void k_lshr64(unsigned* out, int iters) {
+    unsigned long long a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(REP8("v_lshrrev_b64 %0, 3, %0\n v_lshrrev_b64 %1, 3, %1\n"
+                          "v_lshrrev_b64 %2, 3, %2\n v_lshrrev_b64 %3, 3, %3\n"
+                          "v_lshrrev_b64 %0, 5, %0\n v_lshrrev_b64 %1, 5, %1\n"
+                          "v_lshrrev_b64 %2, 5, %2\n v_lshrrev_b64 %3, 5, %3\n")
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3);
+}
+__global__ __launch_bounds__(256) void k_pkmov(unsigned* out, int iters) {
+    unsigned long long a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(REP8("v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]\n v_pk_mov_b32 %1, %1, %1 op_sel:[1,0]\n"
+                          "v_pk_mov_b32 %2, %2, %2 op_sel:[1,0]\n v_pk_mov_b32 %3, %3, %3 op_sel:[1,0]\n"
+                          "v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]\n v_pk_mov_b32 %1, %1, %1 op_sel:[1,0]\n"
+                          "v_pk_mov_b32 %2, %2, %2 op_sel:[1,0]\n v_pk_mov_b32 %3, %3, %3 op_sel:[1,0]\n")
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3);
+}
 
 // 64-bit add forms used by SHA-512.
 __global__ __launch_bounds__(256) void k_lshl_add_u64(unsigned* out, int iters) {
@@ -78,7 +117,10 @@ int main() {
         {"v_bitop3_b32", k_bitop3, 64}, {"v_xor_b32", k_xor, 64}, {"v_perm_b32", k_perm, 64},
         {"v_lshl_add_u32", k_lshladd, 64}, {"v_bfe_u32", k_bfe, 64}, {"v_xad_u32", k_xad, 64},
         {"v_fma_f32", k_fma, 64}, {"v_lshl_add_u64", k_lshl_add_u64, 64},
-        {"v_add_co+addc (per instr)", k_addc_pair, 64}};
+        {"v_add_co+addc (per instr)", k_addc_pair, 64},
+        {"v_lshlrev_b32", k_shl, 64}, {"v_lshrrev_b32", k_shr, 64}, {"v_lshl_or_b32", k_lshlor, 64},
+        {"v_alignbyte_b32", k_alignbyte, 64}, {"v_mov_b32", k_mov, 64}, {"v_bfi_b32", k_bfi, 64},
+        {"v_or3_b32", k_or3, 64}, {"v_lshrrev_b64", k_lshr64, 64}, {"v_pk_mov_b32", k_pkmov, 64}};
     int dev;
     hipGetDevice(&dev);
     int clk_khz;
