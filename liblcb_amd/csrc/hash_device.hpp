@@ -96,6 +96,21 @@ __device__ __forceinline__ u64p xor3p(u64p a, u64p b, u64p c) {
     return u64p{xor3(a.lo, b.lo, c.lo), xor3(a.hi, b.hi, c.hi)};
 }
 __device__ __forceinline__ u64p add64p(u64p a, u64p b) { return mk64(v64(a) + v64(b)); }
+// 64-bit add as one v_lshl_add_u64 on register pairs.  Written as asm because
+// the compiler otherwise splits ((hi << 32) | lo) + y into a zero-extended low
+// add, a separate 32-bit high add and pair-building moves (measured on the
+// SHA-512 block: 1096 v_lshl_add_u64 + 542 v_mov_b32 + 108 v_add_u32 where
+// 752 adds suffice).
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint64_t add64k(uint64_t a, uint64_t k) {  // k wave-uniform
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "s"(k));
+    return r;
+}
 
 // ------------------------------------------------------- block loading
 // Bytes [p, p+64) of a message that has at least 64 bytes left, as 16 raw LE
@@ -443,16 +458,16 @@ struct Sha512 {
             const u64p w15 = v.w[(i - 15) & 15], w2 = v.w[(i - 2) & 15];
             const u64p s0 = xor3p(rotr64p<1>(w15), rotr64p<8>(w15), shr64p<7>(w15));
             const u64p s1 = xor3p(rotr64p<19>(w2), rotr64p<61>(w2), shr64p<6>(w2));
-            x = mk64(v64(v.w[i & 15]) + v64(s0) + v64(v.w[(i - 7) & 15]) + v64(s1));
+            x = mk64(add64(add64(v64(v.w[i & 15]), v64(s0)), add64(v64(v.w[(i - 7) & 15]), v64(s1))));
             v.w[i & 15] = x;
         }
         const u64p S1 = xor3p(rotr64p<14>(v.e), rotr64p<18>(v.e), rotr64p<41>(v.e));
         const u64p ch = u64p{ch3(v.e.lo, v.f.lo, v.g.lo), ch3(v.e.hi, v.f.hi, v.g.hi)};
-        const uint64_t t1 = v64(v.h) + v64(S1) + v64(ch) + kSha512Kc[i] + v64(x);
+        const uint64_t t1 = add64(add64(add64k(v64(v.h), kSha512Kc[i]), v64(x)), add64(v64(S1), v64(ch)));
         const u64p S0 = xor3p(rotr64p<28>(v.a), rotr64p<34>(v.a), rotr64p<39>(v.a));
         const u64p mj = u64p{maj3(v.a.lo, v.b.lo, v.c.lo), maj3(v.a.hi, v.b.hi, v.c.hi)};
-        v.h = v.g; v.g = v.f; v.f = v.e; v.e = mk64(v64(v.d) + t1); v.d = v.c; v.c = v.b; v.b = v.a;
-        v.a = mk64(t1 + v64(S0) + v64(mj));
+        v.h = v.g; v.g = v.f; v.f = v.e; v.e = mk64(add64(v64(v.d), t1)); v.d = v.c; v.c = v.b; v.b = v.a;
+        v.a = mk64(add64(t1, add64(v64(S0), v64(mj))));
     }
     template <int... I>
     __device__ __forceinline__ static void rounds(Vars& v, std::integer_sequence<int, I...>) {

@@ -19,6 +19,7 @@ p.add_argument("--alg", default="md5")
 p.add_argument("--reps", type=int, default=10)
 p.add_argument("--count", type=int, default=1 << 20)
 p.add_argument("--len", type=int, default=1024)
+p.add_argument("--warmup", type=int, default=60, help="untimed launches per algorithm (clock ramp)")
 a = p.parse_args()
 
 data = liblcb_amd.gen_synthetic(0x6C62636861736821, a.count * a.len)
@@ -27,6 +28,9 @@ for name in a.alg.split(","):
     alg = ALG_IDS[name]
     dig = torch.empty((a.count, DIGEST_SIZE[alg]), dtype=torch.uint8, device="cuda")
     ts = []
+    for _ in range(a.warmup):
+        check(lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), None, None, a.count, a.len, a.len,
+                                   dig.data_ptr(), F_DEVICE, s.cuda_stream))
     for r in range(a.reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
