@@ -61,6 +61,42 @@ SIGNATURES = [
 ]
 
 
+class QueueSettings(ctypes.Structure):
+    """lcb_hash_queue_settings_t (include/lcb_hash_queue.h)."""
+    _fields_ = [("max_batch_msgs", c_sz), ("max_batch_bytes", c_sz), ("flush_usec", c_u32),
+                ("batches", c_u32), ("align", c_u32), ("flags", c_u32)]
+
+
+class QueueStats(ctypes.Structure):
+    """lcb_hash_queue_stats_t."""
+    _fields_ = [(n, c_u64) for n in ("packets", "bytes", "batches", "sealed_full", "sealed_timer",
+                                     "sealed_flush", "max_batch_msgs", "submit_waits")]
+
+
+class Seg(ctypes.Structure):
+    """lcb_hash_seg_t."""
+    _fields_ = [("data", c_vp), ("size", c_sz)]
+
+
+# void cb(void *udata, int error, const uint8_t *digest, size_t digest_size)
+DONE_CB = ctypes.CFUNCTYPE(None, c_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), c_sz)
+Q_F_NOWAIT = 0x1
+
+# every symbol include/lcb_hash_queue.h declares
+QUEUE_SIGNATURES = [
+    ("lcb_hash_queue_settings_def", None, [ctypes.POINTER(QueueSettings)]),
+    ("lcb_hash_queue_create", ctypes.c_int,
+     [ctypes.c_int, c_vp, c_sz, ctypes.POINTER(QueueSettings), ctypes.POINTER(c_vp)]),
+    ("lcb_hash_queue_destroy", None, [c_vp]),
+    ("lcb_hash_queue_submit", ctypes.c_int, [c_vp, c_vp, c_sz, c_vp, DONE_CB, c_vp, c_u32]),
+    ("lcb_hash_queue_submitv", ctypes.c_int,
+     [c_vp, ctypes.POINTER(Seg), c_sz, c_vp, DONE_CB, c_vp, c_u32]),
+    ("lcb_hash_queue_flush", ctypes.c_int, [c_vp]),
+    ("lcb_hash_queue_wait", ctypes.c_int, [c_vp]),
+    ("lcb_hash_queue_stats", ctypes.c_int, [c_vp, ctypes.POINTER(QueueStats)]),
+]
+
+
 class LcbHashError(OSError):
     """A non-zero liblcb-style errno from the C-ABI."""
 
@@ -73,7 +109,7 @@ def lib():
             raise RuntimeError("%s is missing: build it with `python -c 'import __graft_entry__ as g; "
                                "g.build()'` (or `make -C liblcb_amd`)" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES:
+        for name, res, args in SIGNATURES + QUEUE_SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

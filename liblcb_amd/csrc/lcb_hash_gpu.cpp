@@ -20,9 +20,7 @@
 #include "../../include/lcb_hash_gpu.h"
 #include "lcb_internal.hpp"
 
-using namespace lcbgpu;
-
-namespace {
+namespace lcbgpu {
 
 size_t dsize(int alg) {
     static const size_t ds[9] = {0, 16, 20, 28, 32, 48, 64, 32, 64};
@@ -90,6 +88,23 @@ int launch_ordered(int alg, KArgs a, hipStream_t s) {
     if (work) (void)hipFreeAsync(work, s);
     return map_err(e);
 }
+
+std::once_flag g_init_flag;
+int g_init_rc = 0;
+
+int ensure_init() {
+    std::call_once(g_init_flag, [] {
+        int n = 0;
+        g_init_rc = (hipGetDeviceCount(&n) != hipSuccess || n <= 0) ? ENODEV : 0;
+    });
+    return g_init_rc;
+}
+
+}  // namespace lcbgpu
+
+using namespace lcbgpu;
+
+namespace {
 
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
@@ -344,9 +359,6 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     return rc3;
 }
 
-std::once_flag g_init_flag;
-int g_init_rc = 0;
-
 }  // namespace
 
 // ================================================================== ABI
@@ -369,6 +381,8 @@ const char* lcb_hash_strerror(int error) {
     case ENOMEM: return "out of device or pinned memory";
     case ENODEV: return "no usable MI355X / HIP device";
     case EIO: return "HIP launch or copy failure";
+    case EMSGSIZE: return "packet larger than a queue batch";
+    case EAGAIN: return "no free queue staging slot";
     default: return "unknown error";
     }
 }
@@ -381,11 +395,7 @@ int lcb_hash_batch(int alg, const uint8_t* key, size_t key_len, const uint8_t* d
     if (count == 0) return 0;
     if (!data || !digests) return EINVAL;
     if (key == nullptr && key_len != 0) return EINVAL;
-    std::call_once(g_init_flag, [] {
-        int n = 0;
-        g_init_rc = (hipGetDeviceCount(&n) != hipSuccess || n <= 0) ? ENODEV : 0;
-    });
-    if (g_init_rc) return g_init_rc;
+    if (int rc = ensure_init()) return rc;
     if (flags & LCB_HASH_F_DEVICE)
         return batch_device(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len,
                             digests, reinterpret_cast<hipStream_t>(stream));

@@ -39,4 +39,16 @@ void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
 void gost_table_host(uint64_t* out);
 
+// Shared by the C-ABI TUs (lcb_hash_gpu.cpp).
+size_t dsize(int alg);                  // digest bytes, 0 for an unknown alg
+size_t bsize(int alg);                  // block bytes (HMAC key block)
+int map_err(hipError_t e);              // HIP error -> liblcb errno code
+int ensure_init();                      // 0, or ENODEV without a usable device
+// Enqueue the HMAC mid-state prep; *mid / *dkey are stream-ordered
+// allocations the caller releases with hipFreeAsync after its last use.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
+               uint8_t** dkey_out);
+// Batch kernel launch, bucketing a large ragged batch by length first.
+int launch_ordered(int alg, KArgs a, hipStream_t s);
+
 }  // namespace lcbgpu

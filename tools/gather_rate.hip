@@ -7,7 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
-template <int kMode>  // 0: all LDS, 1: all global, 2: 6 LDS + 2 global, 3: 5 LDS + 3 global
+template <int kMode>  // 0: all LDS, 1: all global, 2: 6 LDS + 2 global, 3: 5 LDS + 3 global, 4: 7 LDS + 1 global
 __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ gtab, uint64_t* out, int iters) {
     __shared__ uint64_t T[2048];
     for (int i = threadIdx.x; i < 2048; i += 256) T[i] = gtab[i];
@@ -18,7 +18,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ gta
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const bool glob = (kMode == 1) || (kMode == 2 && c >= 6) || (kMode == 3 && c >= 5);
+            const bool glob = (kMode == 1) || (kMode == 2 && c >= 6) || (kMode == 3 && c >= 5) ||
+                              (kMode == 4 && c >= 7);
             const uint64_t v = glob ? gtab[c * 256 + idx[c]] : T[c * 256 + idx[c]];
             acc ^= v;
             idx[c] = (uint32_t)(v >> (8 * (it & 7))) & 255;
@@ -39,9 +40,9 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     const int iters = 512;
-    const char* names[4] = {"lds", "global(L1)", "6 lds+2 glob", "5 lds+3 glob"};
+    const char* names[5] = {"lds", "global(L1)", "6 lds+2 glob", "5 lds+3 glob", "7 lds+1 glob"};
     for (int pass = 0; pass < 2; ++pass)
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < 5; ++m) {
             float best = 1e9;
             for (int r = 0; r < 5; ++r) {
                 hipEventRecord(a, 0);
@@ -49,6 +50,7 @@ int main() {
                 if (m == 1) hipLaunchKernelGGL(k_gather<1>, dim3(blocks), dim3(256), 0, 0, gtab, out, iters);
                 if (m == 2) hipLaunchKernelGGL(k_gather<2>, dim3(blocks), dim3(256), 0, 0, gtab, out, iters);
                 if (m == 3) hipLaunchKernelGGL(k_gather<3>, dim3(blocks), dim3(256), 0, 0, gtab, out, iters);
+                if (m == 4) hipLaunchKernelGGL(k_gather<4>, dim3(blocks), dim3(256), 0, 0, gtab, out, iters);
                 hipEventRecord(b, 0);
                 if (hipEventSynchronize(b) != hipSuccess || hipGetLastError() != hipSuccess) {
                     printf("failed\n");

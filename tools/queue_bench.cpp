@@ -1,0 +1,168 @@
+// queue_bench.cpp — throughput and latency of the asynchronous ingestion queue
+// (include/lcb_hash_queue.h) with native producer threads, the way a
+// thread pool's packet callbacks would feed it.
+//
+// Packets: packet i = `size` bytes at pool + i*size, pool = the splitmix64
+// stream of SURVEY.md §8d (byte b = byte (b&7) of mix64(seed ^ (b>>3))), so
+// the digests are reproducible by oracle/pyoracle.gen_stream.
+//
+// Output: one JSON line {packets, bytes, seconds, packets_per_s, GiB_s,
+// lat_us_p50/p99/max (submit -> callback), queue stats}
+// and, with --out FILE, the packed digests (for the oracle comparison).
+//
+// usage: queue_bench [--alg 1] [--packets 1048576] [--size 1024] [--threads 8]
+//                    [--flush-us 200] [--batch-msgs 65536] [--batch-bytes 67108864]
+//                    [--slots 4] [--key HEX] [--out FILE]
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/lcb_hash_gpu.h"
+#include "../include/lcb_hash_queue.h"
+
+static uint64_t mix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Ctx {
+    std::vector<int64_t>* t_sub;
+    std::vector<int64_t>* t_done;
+    std::atomic<uint64_t>* errors;
+};
+static Ctx g_ctx;
+
+// Completion callback (runs on the queue's completion thread); udata is the
+// packet index.
+static void on_done(void* udata, int error, const uint8_t*, size_t) {
+    const uint64_t i = (uint64_t)(uintptr_t)udata;
+    (*g_ctx.t_done)[i] = now_ns();
+    if (error) g_ctx.errors->fetch_add(1);
+}
+
+int main(int argc, char** argv) {
+    int alg = 1, threads = 8;
+    uint64_t packets = 1 << 20, size = 1024, seed = 0x6C62636861736821ull;
+    lcb_hash_queue_settings_t cfg;
+    lcb_hash_queue_settings_def(&cfg);
+    cfg.max_batch_bytes = 64u << 20;
+    std::string keyhex, out;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        std::string a = argv[i], v = argv[i + 1];
+        if (a == "--alg") alg = atoi(v.c_str());
+        else if (a == "--packets") packets = strtoull(v.c_str(), nullptr, 0);
+        else if (a == "--size") size = strtoull(v.c_str(), nullptr, 0);
+        else if (a == "--threads") threads = atoi(v.c_str());
+        else if (a == "--flush-us") cfg.flush_usec = (uint32_t)atoi(v.c_str());
+        else if (a == "--batch-msgs") cfg.max_batch_msgs = strtoull(v.c_str(), nullptr, 0);
+        else if (a == "--batch-bytes") cfg.max_batch_bytes = strtoull(v.c_str(), nullptr, 0);
+        else if (a == "--slots") cfg.batches = (uint32_t)atoi(v.c_str());
+        else if (a == "--align") cfg.align = (uint32_t)atoi(v.c_str());
+        else if (a == "--key") keyhex = v;
+        else if (a == "--out") out = v;
+        else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
+    }
+    const size_t D = lcb_hash_digest_size(alg);
+    if (!D || threads < 1 || threads > 64) { fprintf(stderr, "bad arguments\n"); return 2; }
+    std::vector<uint8_t> key;
+    for (size_t k = 0; k + 1 < keyhex.size(); k += 2) key.push_back((uint8_t)strtoul(keyhex.substr(k, 2).c_str(), nullptr, 16));
+
+    // Packet pool (the synthetic stream), generated in parallel.
+    const uint64_t nbytes = packets * size;
+    std::vector<uint8_t> pool(nbytes + 8);
+    {
+        std::vector<std::thread> th;
+        const uint64_t words = (nbytes + 7) / 8;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                for (uint64_t w = words * t / threads; w < words * (t + 1) / threads; ++w) {
+                    const uint64_t v = mix64(seed ^ w);
+                    memcpy(&pool[w * 8], &v, 8);
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<uint8_t> digests(packets * D);
+    std::vector<int64_t> t_sub(packets), t_done(packets);
+    std::atomic<uint64_t> errors{0};
+    g_ctx = Ctx{&t_sub, &t_done, &errors};
+
+    lcb_hash_queue_p q = nullptr;
+    int rc = lcb_hash_queue_create(alg, key.empty() && keyhex.empty() ? nullptr : key.data(), key.size(), &cfg, &q);
+    if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
+
+    // Warm-up: one batch through the whole pipeline (first launch, clocks).
+    {
+        std::vector<uint8_t> wd(std::min<uint64_t>(packets, 4096) * D);
+        for (uint64_t i = 0; i < wd.size() / D; ++i)
+            lcb_hash_queue_submit(q, &pool[i * size], size, &wd[i * D], nullptr, nullptr, 0);
+        lcb_hash_queue_wait(q);
+    }
+    lcb_hash_queue_stats_t st0;
+    lcb_hash_queue_stats(q, &st0);
+
+    std::atomic<int> fail{0};
+    const int64_t t0 = now_ns();
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                const uint64_t lo = packets * t / threads, hi = packets * (t + 1) / threads;
+                for (uint64_t i = lo; i < hi; ++i) {
+                    t_sub[i] = now_ns();
+                    int r = lcb_hash_queue_submit(q, &pool[i * size], size, &digests[i * D], on_done,
+                                                  (void*)(uintptr_t)i, 0);
+                    if (r) { fail.store(r); return; }
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    rc = lcb_hash_queue_wait(q);
+    const int64_t t1 = now_ns();
+    lcb_hash_queue_stats_t st;
+    lcb_hash_queue_stats(q, &st);
+    lcb_hash_queue_destroy(q);
+    if (fail.load() || rc || errors.load()) {
+        fprintf(stderr, "failed: submit %d wait %d cb-errors %llu\n", fail.load(), rc,
+                (unsigned long long)errors.load());
+        return 1;
+    }
+    std::vector<double> lat(packets);
+    for (uint64_t i = 0; i < packets; ++i) lat[i] = (t_done[i] - t_sub[i]) * 1e-3;
+    std::sort(lat.begin(), lat.end());
+    const double sec = (t1 - t0) * 1e-9;
+    printf("{\"alg\": %d, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"flush_usec\": %u, "
+           "\"batch_msgs\": %llu, \"batch_bytes\": %llu, \"slots\": %u, \"seconds\": %.4f, "
+           "\"packets_per_s\": %.0f, \"GiB_s\": %.3f, \"lat_us_p50\": %.1f, \"lat_us_p99\": %.1f, "
+           "\"lat_us_max\": %.1f, \"batches\": %llu, \"sealed_full\": %llu, \"sealed_timer\": %llu, "
+           "\"sealed_flush\": %llu, \"submit_waits\": %llu}\n",
+           alg, (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
+           (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, sec,
+           packets / sec, nbytes / sec / (1ull << 30), lat[packets / 2], lat[packets * 99 / 100],
+           lat[packets - 1], (unsigned long long)(st.batches - st0.batches),
+           (unsigned long long)(st.sealed_full - st0.sealed_full),
+           (unsigned long long)(st.sealed_timer - st0.sealed_timer),
+           (unsigned long long)(st.sealed_flush - st0.sealed_flush),
+           (unsigned long long)(st.submit_waits - st0.submit_waits));
+    if (!out.empty()) {
+        FILE* f = fopen(out.c_str(), "wb");
+        if (!f || fwrite(digests.data(), 1, digests.size(), f) != digests.size()) return 1;
+        fclose(f);
+    }
+    return 0;
+}
