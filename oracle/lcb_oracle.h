@@ -62,6 +62,23 @@ int or_batch(int alg, const uint8_t *key, size_t key_len,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
     size_t count, uint64_t stride, uint32_t fixed_len, uint8_t *digests);
 
+/*
+ * CRC-32 family of include/math/crc32.h (oracle/crc32_oracle.c).  Variant
+ * ids are shared with include/lcb_crc32_gpu.h.
+ */
+enum {
+	OR_CRC32A = 1, OR_CRC32CKSUM = 2, OR_CRC32MPEG2 = 3, OR_CRC32B = 4,
+	OR_CRC32JAMCRC = 5, OR_CRC32C = 6, OR_CRC32D = 7, OR_CRC32Q = 8
+};
+int      or_crc32_valid(int variant);
+uint32_t or_crc32_table(int variant, int i);	/* byte table entry */
+uint32_t or_crc32_update(int variant, uint32_t crc, const uint8_t *d, size_t n);
+uint32_t or_crc32(int variant, const uint8_t *d, size_t n);
+/* init == NULL: crcs[i] = X(msg i); else crcs[i] = X_update(init[i], msg i). */
+int or_crc32_batch(int variant, const uint32_t *init, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lengths, size_t count,
+    uint64_t stride, uint32_t fixed_len, uint32_t *crcs);
+
 /* Synthetic-input generator: byte b of the stream is byte
  * (b & 7) of splitmix64_mix(seed ^ (b >> 3)).  Writes n bytes starting at
  * stream byte position `start`. */

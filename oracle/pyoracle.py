@@ -89,7 +89,39 @@ _ARGS = [_c.c_int, _c.c_char_p, _c.c_size_t, _c.c_void_p, _c.c_void_p, _c.c_void
          _c.c_size_t, _c.c_uint64, _c.c_uint32, _c.c_void_p]
 
 
-class Oracle(_Batch):
+_CRC_ARGS = [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+             _c.c_uint64, _c.c_uint32, _c.c_void_p]
+CRC_VARIANTS = {1: "crc32a", 2: "crc32cksum", 3: "crc32mpeg2", 4: "crc32b", 5: "crc32jamcrc",
+                6: "crc32c", 7: "crc32d", 8: "crc32q"}
+
+
+class _Crc:
+    fn_crc = None
+
+    def crc32_batch(self, variant, data, offsets=None, lengths=None, count=None, stride=0,
+                    fixed_len=0, init=None):
+        """crcs[i] = X(msg i), or X_update(init[i], msg i) (include/math/crc32.h)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if count is None:
+            count = len(lengths) if lengths is not None else len(offsets)
+        if init is not None:
+            init = np.ascontiguousarray(init, dtype=np.uint32)
+        out = np.zeros(count, dtype=np.uint32)
+        rc = self.fn_crc(variant, init.ctypes.data if init is not None else None, data.ctypes.data,
+                         offsets.ctypes.data if offsets is not None else None,
+                         lengths.ctypes.data if lengths is not None else None,
+                         count, stride, fixed_len, out.ctypes.data)
+        assert rc == 0, rc
+        return out
+
+
+class Oracle(_Batch, _Crc):
     """The C restatement."""
 
     def __init__(self, path=ORACLE_SO):
@@ -101,6 +133,13 @@ class Oracle(_Batch):
         self.lib.or_init.argtypes = [_c.c_void_p, _c.c_int]
         self.lib.or_update.argtypes = [_c.c_void_p, _c.c_char_p, _c.c_size_t]
         self.lib.or_final.argtypes = [_c.c_void_p, _c.c_char_p]
+        self.lib.or_crc32_batch.argtypes = _CRC_ARGS
+        self.fn_crc = self.lib.or_crc32_batch
+        self.lib.or_crc32_table.restype = _c.c_uint32
+        self.lib.or_crc32_table.argtypes = [_c.c_int, _c.c_int]
+
+    def crc32_table(self, variant):
+        return np.array([self.lib.or_crc32_table(variant, i) for i in range(256)], np.uint32)
 
     def chunked(self, alg, msg, chunks):
         """Streaming digest feeding `msg` in pieces of the given size."""
@@ -116,7 +155,7 @@ class Oracle(_Batch):
         return out.raw[:DSIZE[alg]]
 
 
-class Ref(_Batch):
+class Ref(_Batch, _Crc):
     """The reference's own code (compiled from /root/reference into _ref/)."""
 
     def __init__(self, path=REF_SO):
@@ -124,6 +163,17 @@ class Ref(_Batch):
         self.lib.ref_batch.argtypes = _ARGS
         self.fn_batch = self.lib.ref_batch
         self.lib.ref_gost_ax.argtypes = [_c.c_void_p]
+        self.lib.ref_crc32_batch.argtypes = _CRC_ARGS
+        self.fn_crc = self.lib.ref_crc32_batch
+        self.lib.ref_crc32_table.argtypes = [_c.c_int, _c.c_void_p]
+
+    def crc32_table(self, variant):
+        t = np.zeros(256, np.uint32)
+        assert self.lib.ref_crc32_table(variant, t.ctypes.data) == 0
+        return t
+
+    def crc32_self_test(self):
+        return self.lib.ref_crc32_self_test()
 
     @staticmethod
     def available(path=REF_SO):

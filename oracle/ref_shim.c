@@ -35,6 +35,12 @@
 #include "crypto/hash/sha2.h"
 #include "crypto/hash/gost3411-2012.h"
 
+#ifndef nitems			/* BSD sys/param.h macro used by crc32.h:619 */
+#	define nitems(x)	(sizeof((x)) / sizeof((x)[0]))
+#endif
+#define CRC32_SELF_TEST 1
+#include "math/crc32.h"
+
 enum { A_MD5 = 1, A_SHA1, A_SHA224, A_SHA256, A_SHA384, A_SHA512, A_GOST256, A_GOST512 };
 
 static size_t
@@ -142,4 +148,61 @@ int
 ref_gost_ax(uint64_t *out /* 8*256 */) {
 	memcpy(out, gost3411_2012_Ax, sizeof(gost3411_2012_Ax));
 	return (int)sizeof(gost3411_2012_Ax);
+}
+
+/* ---------------------------------------------------------------- CRC-32
+ * include/math/crc32.h, variant ids as include/lcb_crc32_gpu.h:
+ * 1 crc32a, 2 cksum, 3 mpeg2, 4 crc32b, 5 jamcrc, 6 crc32c, 7 crc32d, 8 crc32q. */
+int
+ref_crc32_self_test(void) {
+	return crc32_self_test();	/* crc32.h:581-657 */
+}
+
+static uint32_t
+ref_crc32_one(int v, int upd, uint32_t c, const uint8_t *p, size_t n) {
+	switch (v) {
+	case 1: return upd ? crc32a_update(c, p, n) : crc32a(p, n);
+	case 2: return upd ? crc32cksum_update(c, p, n) : crc32cksum(p, n);
+	case 3: return upd ? crc32mpeg2_update(c, p, n) : crc32mpeg2(p, n);
+	case 4: return upd ? crc32b_update(c, p, n) : crc32b(p, n);
+	case 5: return upd ? crc32jamcrc_update(c, p, n) : crc32jamcrc(p, n);
+	case 6: return upd ? crc32c_update(c, p, n) : crc32c(p, n);
+	case 7: return upd ? crc32d_update(c, p, n) : crc32d(p, n);
+	case 8: return upd ? crc32q_update(c, p, n) : crc32q(p, n);
+	}
+	return 0;
+}
+
+/* init == NULL: crcs[i] = X(msg i); else X_update(init[i], msg i). */
+int
+ref_crc32_batch(int v, const uint32_t *init, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lengths, size_t count,
+    uint64_t stride, uint32_t fixed_len, uint32_t *crcs) {
+	size_t i;
+
+	if (v < 1 || v > 8)
+		return -1;
+	for (i = 0; i < count; i ++) {
+		const uint8_t *p = base + (offsets ? offsets[i] : (uint64_t)i * stride);
+		size_t n = (lengths ? lengths[i] : fixed_len);
+		crcs[i] = ref_crc32_one(v, init != NULL, init ? init[i] : 0, p, n);
+	}
+	return 0;
+}
+
+/* The reference's 256-entry byte table used by variant v (crc32.h:128-494). */
+int
+ref_crc32_table(int v, uint32_t *out) {
+	const uint32_t *t;
+
+	switch (v) {
+	case 1: case 2: case 3: t = crc32_tbl256_04c11db7; break;
+	case 4: case 5: t = crc32_tbl256_edb88320; break;
+	case 6: t = crc32_tbl256_1edc6f41; break;
+	case 7: t = crc32_tbl256_a833982b; break;
+	case 8: t = crc32_tbl256_814141ab; break;
+	default: return -1;
+	}
+	memcpy(out, t, 256 * sizeof(uint32_t));
+	return 0;
 }
