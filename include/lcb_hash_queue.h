@@ -74,6 +74,10 @@ typedef struct lcb_hash_queue_stats_s {
 	uint64_t	sealed_flush;	/* ... sealed by flush()/wait(). */
 	uint64_t	max_batch_msgs;	/* Largest launched batch. */
 	uint64_t	submit_waits;	/* Submits that had to wait for a slot. */
+	uint64_t	flusher_drain_ns; /* Flusher: waiting for leases, filling holes. */
+	uint64_t	flusher_launch_ns; /* Flusher: enqueueing copies and kernels. */
+	uint64_t	completer_busy_ns; /* Completer: digest copies + callbacks. */
+	uint64_t	gpu_wait_ns;	/* Completer: waiting for launched batches. */
 } lcb_hash_queue_stats_t;
 
 /* Submit flags. */

@@ -70,7 +70,9 @@ class QueueSettings(ctypes.Structure):
 class QueueStats(ctypes.Structure):
     """lcb_hash_queue_stats_t."""
     _fields_ = [(n, c_u64) for n in ("packets", "bytes", "batches", "sealed_full", "sealed_timer",
-                                     "sealed_flush", "max_batch_msgs", "submit_waits")]
+                                     "sealed_flush", "max_batch_msgs", "submit_waits",
+                                     "flusher_drain_ns", "flusher_launch_ns", "completer_busy_ns",
+                                     "gpu_wait_ns")]
 
 
 class Seg(ctypes.Structure):

@@ -3,15 +3,19 @@
 // Structure:
 //   slots      `batches` staging slots, each a page-locked arena (data,
 //              offsets, lengths, digests) + its HBM mirror + a stream/event.
-//   open       the slot producers currently append to.  A producer reserves
-//              (count, bytes) with one CAS on the slot's 64-bit state word
-//              [sealed:1 | count:23 | bytes:40], copies its packet outside any
-//              lock, and leaves; `writers` counts producers between their
-//              reservation and the end of their copy.
-//   flusher    seals the open slot (full / flush_usec / flush request), waits
-//              for writers to drain, installs a free slot as the new open one,
-//              and enqueues H2D -> batch kernel -> D2H on the sealed slot's
-//              stream.
+//   open       the slot producers currently append to.
+//   leases     a producer thread reserves a LEASE of `lease_msgs` message
+//              indices and a run of arena bytes with one CAS on the slot's
+//              state word [sealed:1 | count:23 | bytes:40], then fills it
+//              packet by packet without writing shared cache lines: per packet
+//              it raises/lowers its lease record's `busy` flag around the copy
+//              (a Dekker handshake with the flusher's seal) and publishes
+//              `done` (packets written).  Indices a lease did not fill become
+//              holes: zero-length entries that nobody waits for.
+//   flusher    seals the open slot (full / flush_usec / flush request),
+//              installs a free slot as the new open one at once, then waits
+//              for the sealed slot's leases to go idle, turns their unused
+//              indices into holes and enqueues H2D -> batch kernel -> D2H.
 //   completer  waits for launched slots in order, hands each digest to its
 //              submitter (copy to `digest`, then `cb`), returns the slot.
 //
@@ -32,6 +36,7 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include "../../include/lcb_hash_gpu.h"
@@ -50,6 +55,8 @@ constexpr uint64_t kBytesMask = (1ull << kCountShift) - 1;
 constexpr uint64_t kCountMask = (1ull << 23) - 1;
 constexpr size_t kMaxMsgs = kCountMask;          // per batch
 constexpr size_t kMaxBytes = 1ull << 36;         // per batch (64 GiB)
+constexpr uint32_t kLeaseMsgs = 32;              // message indices per lease
+constexpr size_t kLeaseBytes = 32u << 10;        // arena bytes per lease, at least
 
 inline uint64_t st_count(uint64_t s) { return (s >> kCountShift) & kCountMask; }
 inline uint64_t st_bytes(uint64_t s) { return s & kBytesMask; }
@@ -58,32 +65,79 @@ struct Meta {
     uint8_t* digest;
     lcb_hash_done_cb cb;
     void* udata;
+    uint32_t real;          // 0: hole (index reserved by a lease, never filled)
+};
+
+struct alignas(64) LeaseRec {
+    std::atomic<uint32_t> busy{0};   // producer is between its seal check and publish
+    std::atomic<uint32_t> done{0};   // packets written into this lease
 };
 
 enum SealWhy { kSealFull = 1, kSealTimer = 2, kSealFlush = 3 };
 
 struct Slot {
-    std::atomic<uint64_t> state{0};
-    std::atomic<int> writers{0};
-    std::atomic<int64_t> t_first{0};        // ns since clock epoch of packet 0; 0 = empty
+    alignas(64) std::atomic<uint64_t> state{0};
+    alignas(64) std::atomic<uint32_t> gen{0};    // bumped each time the slot reopens
+    std::atomic<uint32_t> closed{0};             // read-mostly copy of the seal for lease holders
+    std::atomic<int64_t> t_first{0};             // ns timestamp of the first packet; 0 = none
+    uint64_t seq = 0;                            // open order (wait() bookkeeping)
     uint8_t* h_data = nullptr;
     uint64_t* h_off = nullptr;
     uint32_t* h_len = nullptr;
     uint8_t* h_dig = nullptr;
     Meta* meta = nullptr;
+    LeaseRec* leases = nullptr;
+    size_t nleases = 0;
     uint8_t* d_data = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
     uint8_t* d_dig = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    size_t n = 0, bytes = 0, payload = 0;   // final shape of a sealed batch
+    size_t n = 0, bytes = 0, payload = 0, packets = 0;  // final shape of a sealed batch
     int launch_err = 0;
 };
+
+// Copy into the staging arena with streaming stores: the arena is only read
+// again by the DMA engine, so write-allocating its lines in the producer's
+// cache (a read for ownership per line) is wasted memory traffic.  `dst`
+// 16-byte aligned; the caller fences (sfence) before publishing.
+inline void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    if (n < 256 || (reinterpret_cast<uintptr_t>(dst) & 15)) {
+        memcpy(dst, src, n);
+        return;
+    }
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    if (i < n) memcpy(dst + i, src + i, n - i);
+}
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
 }
+
+// A producer thread's current lease in one queue.
+struct Lease {
+    uint64_t qid = 0;           // queue identity (0 = unused entry)
+    Slot* slot = nullptr;
+    uint32_t gen = 0;
+    uint32_t rec = 0;
+    uint64_t idx = 0, idx_end = 0;
+    uint64_t pos = 0, pos_end = 0;
+    bool valid = false;
+};
+constexpr int kTlsLeases = 8;
+thread_local Lease t_leases[kTlsLeases];
+std::atomic<uint64_t> g_next_qid{1};
 
 }  // namespace
 
@@ -91,6 +145,9 @@ struct lcb_hash_queue_s {
     int alg = 0;
     size_t D = 0;
     int device = 0;
+    uint64_t qid = 0;
+    uint32_t lease_msgs = 0;
+    size_t lease_bytes = 0;
     lcb_hash_queue_settings_t cfg{};
     std::vector<Slot> slots;
     uint32_t* mid = nullptr;                 // HMAC mid-states (device), or null
@@ -100,55 +157,92 @@ struct lcb_hash_queue_s {
     std::condition_variable cv_flusher;      // flusher: work may be due
     std::condition_variable cv_open;         // producers: a new open slot
     std::condition_variable cv_complete;     // completer: a slot was launched
-    std::condition_variable cv_done;         // waiters: packets completed
+    std::condition_variable cv_done;         // waiters: a slot completed
     std::condition_variable cv_free;         // flusher: a slot was returned
     std::deque<Slot*> free_slots, inflight;
     bool stop = false;                       // flusher: drain the open slot and exit
     bool completer_stop = false;             // completer: exit once inflight is empty
     std::atomic<bool> flush_req{false};
+    uint64_t next_seq = 1;                   // under m
+    std::atomic<uint64_t> completed_seq{0};  // seq of the last completed slot
 
-    std::atomic<uint64_t> submitted{0}, completed{0}, completed_bytes{0};
+    std::atomic<uint64_t> completed{0}, completed_bytes{0};
     std::atomic<uint64_t> batches{0}, sealed_full{0}, sealed_timer{0}, sealed_flush{0};
     std::atomic<uint64_t> max_batch{0}, submit_waits{0};
+    std::atomic<uint64_t> drain_ns{0}, launch_ns{0}, completer_ns{0}, gpu_wait_ns{0};
     std::atomic<int> first_error{0};
 
     std::thread flusher, completer;
 
     void flusher_main();
     void completer_main();
+    void drain_leases(Slot* b);
     void launch(Slot* b, int why);
     void release_all();
+    void install_open(Slot* b);      // under m
 };
 
 namespace {
 
-// Seal `b` (idempotent); returns true if this call sealed it.
+// Seal `b` (idempotent); returns true if this call sealed it.  The sealed bit
+// in `state` stops new leases; `closed` (a line lease holders only read) stops
+// packets in existing leases.  Its seq_cst store is the sealer's half of the
+// Dekker handshake with `busy` (drain_leases reads `busy` after it).
 bool seal(Slot* b) {
-    uint64_t s = b->state.load(std::memory_order_acquire);
+    uint64_t s = b->state.load(std::memory_order_seq_cst);
+    bool mine = false;
     while (!(s & kSealed))
-        if (b->state.compare_exchange_weak(s, s | kSealed, std::memory_order_acq_rel)) return true;
-    return false;
-}
-
-// Reopen a drained slot.  `writers` is NOT reset: a producer holding a stale
-// pointer to this slot may have incremented it and will decrement it again.
-void reset_slot(Slot* b) {
-    b->t_first.store(0, std::memory_order_relaxed);
-    b->n = b->bytes = b->payload = 0;
-    b->launch_err = 0;
-    b->state.store(0, std::memory_order_release);
+        if (b->state.compare_exchange_weak(s, s | kSealed, std::memory_order_seq_cst)) { mine = true; break; }
+    b->closed.store(1, std::memory_order_seq_cst);
+    return mine;
 }
 
 }  // namespace
 
-// Enqueue one sealed, writer-free slot: H2D, kernel, D2H, completion event.
+// Reopen a drained slot as a new generation (under m).
+void lcb_hash_queue_s::install_open(Slot* b) {
+    for (size_t r = 0; r < b->nleases; ++r) b->leases[r].done.store(0, std::memory_order_relaxed);
+    b->t_first.store(0, std::memory_order_relaxed);
+    b->closed.store(0, std::memory_order_relaxed);
+    b->n = b->bytes = b->payload = b->packets = 0;
+    b->launch_err = 0;
+    b->seq = next_seq++;
+    b->gen.fetch_add(1, std::memory_order_release);
+    b->state.store(0, std::memory_order_release);
+    open.store(b, std::memory_order_release);
+}
+
+// After the seal: wait until no producer is inside any of the slot's leases,
+// then turn every index a lease did not fill into a hole.
+void lcb_hash_queue_s::drain_leases(Slot* b) {
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const uint64_t count = st_count(b->state.load(std::memory_order_acquire));
+    const uint64_t nrec = (count + lease_msgs - 1) / lease_msgs;
+    for (uint64_t r = 0; r < nrec; ++r) {
+        LeaseRec& L = b->leases[r];
+        while (L.busy.load(std::memory_order_seq_cst) != 0) std::this_thread::yield();
+        const uint64_t lo = r * lease_msgs + L.done.load(std::memory_order_acquire);
+        const uint64_t hi = std::min<uint64_t>(count, (r + 1) * lease_msgs);
+        for (uint64_t i = lo; i < hi; ++i) {
+            b->h_off[i] = 0;
+            b->h_len[i] = 0;
+            b->meta[i] = Meta{nullptr, nullptr, nullptr, 0};
+        }
+    }
+}
+
+// Enqueue one sealed, drained slot: H2D, kernel, D2H, completion event.
 void lcb_hash_queue_s::launch(Slot* b, int why) {
     const uint64_t s = b->state.load(std::memory_order_acquire);
     b->n = st_count(s);
     b->bytes = st_bytes(s);
-    size_t payload = 0;
-    for (size_t i = 0; i < b->n; ++i) payload += b->h_len[i];
+    size_t payload = 0, packets = 0;
+    for (size_t i = 0; i < b->n; ++i) {
+        payload += b->h_len[i];
+        packets += b->meta[i].real;
+    }
     b->payload = payload;
+    b->packets = packets;
     hipStream_t st = b->stream;
     KArgs a;
     a.data = b->d_data; a.offsets = b->d_off; a.lengths = b->d_len; a.order = nullptr;
@@ -207,20 +301,22 @@ void lcb_hash_queue_s::flusher_main() {
         }
         seal(b);  // no-op when a producer already sealed it as full
         flush_req.store(false, std::memory_order_release);
-        // Producers that reserved a slot finish their copies.
-        while (b->writers.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-        launch(b, why);
-        // Install the next open slot (waits while every slot is in flight).
-        Slot* next = nullptr;
+        // Reopen first (producers only ever wait for a free slot, never for
+        // the launch below), then drain and launch the sealed slot.
         {
             std::unique_lock<std::mutex> lk(m);
             cv_free.wait(lk, [&] { return !free_slots.empty(); });
-            next = free_slots.front();
+            Slot* next = free_slots.front();
             free_slots.pop_front();
-            reset_slot(next);
-            open.store(next, std::memory_order_release);
+            install_open(next);
         }
         cv_open.notify_all();
+        const int64_t t_busy = now_ns();
+        drain_leases(b);
+        const int64_t t_launch = now_ns();
+        launch(b, why);
+        drain_ns.fetch_add(t_launch - t_busy, std::memory_order_relaxed);
+        launch_ns.fetch_add(now_ns() - t_launch, std::memory_order_relaxed);
     }
 }
 
@@ -234,10 +330,14 @@ void lcb_hash_queue_s::completer_main() {
             if (inflight.empty()) return;
             b = inflight.front();
         }
+        const int64_t t_wait = now_ns();
         int err = b->launch_err;
         if (!err) err = map_err(hipEventSynchronize(b->done));
+        const int64_t t_cb = now_ns();
+        gpu_wait_ns.fetch_add(t_cb - t_wait, std::memory_order_relaxed);
         for (size_t i = 0; i < b->n; ++i) {
             const Meta& mt = b->meta[i];
+            if (!mt.real) continue;
             const uint8_t* dg = b->h_dig + i * D;
             if (!err && mt.digest) memcpy(mt.digest, dg, D);
             if (mt.cb) mt.cb(mt.udata, err, err ? nullptr : dg, D);
@@ -246,12 +346,14 @@ void lcb_hash_queue_s::completer_main() {
             int z = 0;
             first_error.compare_exchange_strong(z, err);
         }
+        completer_ns.fetch_add(now_ns() - t_cb, std::memory_order_relaxed);
+        completed.fetch_add(b->packets, std::memory_order_relaxed);
         completed_bytes.fetch_add(b->payload, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(m);
             inflight.pop_front();
+            completed_seq.store(b->seq, std::memory_order_release);
             free_slots.push_back(b);
-            completed.fetch_add(b->n, std::memory_order_release);
         }
         cv_free.notify_one();
         cv_done.notify_all();
@@ -269,7 +371,7 @@ int validate(const lcb_hash_queue_settings_t& c) {
     return 0;
 }
 
-int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D) {
+int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
 #define Q_TRY(x) do { if ((x) != hipSuccess) return ENOMEM; } while (0)
     Q_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     Q_TRY(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
@@ -283,7 +385,9 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D) {
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_dig), msgs * D));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
-    return b.meta ? 0 : ENOMEM;
+    b.leases = new (std::nothrow) LeaseRec[nleases];
+    b.nleases = nleases;
+    return (b.meta && b.leases) ? 0 : ENOMEM;
 }
 
 void free_slot(Slot& b) {
@@ -298,9 +402,23 @@ void free_slot(Slot& b) {
     if (b.done) (void)hipEventDestroy(b.done);
     if (b.stream) (void)hipStreamDestroy(b.stream);
     delete[] b.meta;
+    delete[] b.leases;
     b.h_data = nullptr; b.h_off = nullptr; b.h_len = nullptr; b.h_dig = nullptr; b.meta = nullptr;
     b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_dig = nullptr;
-    b.done = nullptr; b.stream = nullptr;
+    b.done = nullptr; b.stream = nullptr; b.leases = nullptr; b.nleases = 0;
+}
+
+// This thread's lease entry for queue `qid` (a free or evicted entry if none).
+// Evicting an entry abandons its lease: the unused indices become holes.
+Lease& tls_lease(uint64_t qid) {
+    Lease* victim = &t_leases[qid % kTlsLeases];
+    for (Lease& L : t_leases) {
+        if (L.qid == qid) return L;
+        if (L.qid == 0) victim = &L;
+    }
+    *victim = Lease();
+    victim->qid = qid;
+    return *victim;
 }
 
 }  // namespace
@@ -340,11 +458,15 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
     q->alg = alg;
     q->D = dsize(alg);
     q->cfg = cfg;
+    q->qid = g_next_qid.fetch_add(1);
+    q->lease_msgs = (uint32_t)std::min<size_t>(kLeaseMsgs, cfg.max_batch_msgs);
+    q->lease_bytes = std::min<size_t>(kLeaseBytes, cfg.max_batch_bytes);
     if (hipGetDevice(&q->device) != hipSuccess) { delete q; return ENODEV; }
     q->slots = std::vector<Slot>(cfg.batches);
+    const size_t nleases = (cfg.max_batch_msgs + q->lease_msgs - 1) / q->lease_msgs;
     int rc = 0;
     for (Slot& b : q->slots)
-        if ((rc = alloc_slot(b, cfg.max_batch_msgs, cfg.max_batch_bytes, q->D))) break;
+        if ((rc = alloc_slot(b, cfg.max_batch_msgs, cfg.max_batch_bytes, q->D, nleases))) break;
     if (!rc && key) {
         // HMAC mid-states once per queue (the key is fixed for its lifetime).
         hipStream_t st = q->slots[0].stream;
@@ -369,8 +491,10 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
         return rc;
     }
     for (size_t i = 1; i < q->slots.size(); ++i) q->free_slots.push_back(&q->slots[i]);
-    reset_slot(&q->slots[0]);
-    q->open.store(&q->slots[0], std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->install_open(&q->slots[0]);
+    }
     q->flusher = std::thread([q] { q->flusher_main(); });
     q->completer = std::thread([q] { q->completer_main(); });
     *q_out = q;
@@ -387,59 +511,91 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
     }
     if (len > UINT32_MAX || len > q->cfg.max_batch_bytes) return EMSGSIZE;
     const uint64_t A = q->cfg.align;
+    const uint64_t cap_m = q->cfg.max_batch_msgs, cap_b = q->cfg.max_batch_bytes, LM = q->lease_msgs;
+    Lease& L = tls_lease(q->qid);
     bool waited = false;
     for (;;) {
+        if (L.valid) {
+            Slot* b = L.slot;
+            LeaseRec& r = b->leases[L.rec];
+            // Dekker with the flusher: announce, then check the seal.
+            r.busy.store(1, std::memory_order_relaxed);
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            const bool live = b->gen.load(std::memory_order_relaxed) == L.gen &&
+                              !b->closed.load(std::memory_order_relaxed);
+            const uint64_t pos = (L.pos + A - 1) & ~(A - 1);
+            if (live && L.idx < L.idx_end && pos + len <= L.pos_end) {
+                uint8_t* dst = b->h_data + pos;
+                for (size_t k = 0; k < nsegs; ++k) {
+                    if (segs[k].size) stream_copy(dst, segs[k].data, segs[k].size);
+                    dst += segs[k].size;
+                }
+                _mm_sfence();  // streaming stores before the release of `done`
+                const uint64_t i = L.idx;
+                b->h_off[i] = pos;
+                b->h_len[i] = (uint32_t)len;
+                b->meta[i] = Meta{digest, cb, udata, 1};
+                L.idx = i + 1;
+                L.pos = pos + len;
+                r.done.store((uint32_t)(L.idx - (uint64_t)L.rec * LM), std::memory_order_release);
+                r.busy.store(0, std::memory_order_release);
+                if (b->t_first.load(std::memory_order_relaxed) == 0) {
+                    int64_t z = 0;
+                    if (b->t_first.compare_exchange_strong(z, now_ns(), std::memory_order_acq_rel)) {
+                        { std::lock_guard<std::mutex> lk(q->m); }
+                        q->cv_flusher.notify_one();
+                    }
+                }
+                return 0;
+            }
+            r.busy.store(0, std::memory_order_release);
+            L.valid = false;
+        }
+        // New lease on the open slot: LM indices and room for LM packets of
+        // this size (at least kLeaseBytes), shrunk to what the slot has left.
         Slot* b = q->open.load(std::memory_order_acquire);
-        b->writers.fetch_add(1, std::memory_order_acq_rel);
+        const uint32_t g = b->gen.load(std::memory_order_acquire);
         uint64_t s = b->state.load(std::memory_order_acquire);
-        uint64_t idx = 0, pos = 0;
         bool got = false;
+        uint64_t cnt = 0, pos0 = 0, nbytes = 0;
         while (!(s & kSealed)) {
-            const uint64_t cnt = st_count(s), used = st_bytes(s);
-            pos = (used + A - 1) & ~(A - 1);
-            if (cnt + 1 > q->cfg.max_batch_msgs || pos + len > q->cfg.max_batch_bytes) {
+            cnt = st_count(s);
+            pos0 = (st_bytes(s) + A - 1) & ~(A - 1);
+            const uint64_t room = cap_b > pos0 ? cap_b - pos0 : 0;
+            if (cnt + LM > cap_m || room < len) {  // an empty slot always fits
                 if (seal(b)) {
                     { std::lock_guard<std::mutex> lk(q->m); }
                     q->cv_flusher.notify_one();
                 }
                 break;
             }
-            const uint64_t ns = ((cnt + 1) << kCountShift) | (pos + len);
+            const uint64_t want = std::max<uint64_t>(q->lease_bytes,
+                                                     std::min<uint64_t>(LM * (len + A), cap_b / 8));
+            nbytes = std::min<uint64_t>(std::max<uint64_t>(want, len), room);
+            const uint64_t ns = ((cnt + LM) << kCountShift) | (pos0 + nbytes);
             if (b->state.compare_exchange_weak(s, ns, std::memory_order_acq_rel)) {
-                idx = cnt;
                 got = true;
                 break;
             }
         }
-        if (!got) {
-            // Sealed: wait until the flusher installs a new open slot.
-            b->writers.fetch_sub(1, std::memory_order_release);
-            std::unique_lock<std::mutex> lk(q->m);
-            if (q->open.load(std::memory_order_acquire) == b) {
-                if (flags & LCB_HASH_Q_F_NOWAIT) return EAGAIN;
-                if (!waited) { q->submit_waits.fetch_add(1, std::memory_order_relaxed); waited = true; }
-                q->cv_open.wait(lk, [&] { return q->open.load(std::memory_order_acquire) != b; });
-            }
+        if (got) {
+            L.slot = b;
+            L.gen = g;
+            L.rec = (uint32_t)(cnt / LM);
+            L.idx = cnt;
+            L.idx_end = cnt + LM;
+            L.pos = pos0;
+            L.pos_end = pos0 + nbytes;
+            L.valid = true;
             continue;
         }
-        uint8_t* dst = b->h_data + pos;
-        for (size_t k = 0; k < nsegs; ++k) {
-            if (segs[k].size) memcpy(dst, segs[k].data, segs[k].size);
-            dst += segs[k].size;
+        // Sealed: wait until the flusher installs a new open slot.
+        std::unique_lock<std::mutex> lk(q->m);
+        if (q->open.load(std::memory_order_acquire) == b) {
+            if (flags & LCB_HASH_Q_F_NOWAIT) return EAGAIN;
+            if (!waited) { q->submit_waits.fetch_add(1, std::memory_order_relaxed); waited = true; }
+            q->cv_open.wait(lk, [&] { return q->open.load(std::memory_order_acquire) != b; });
         }
-        b->h_off[idx] = pos;
-        b->h_len[idx] = (uint32_t)len;
-        b->meta[idx] = Meta{digest, cb, udata};
-        q->submitted.fetch_add(1, std::memory_order_relaxed);
-        if (idx == 0) {
-            b->t_first.store(now_ns(), std::memory_order_release);
-            b->writers.fetch_sub(1, std::memory_order_release);
-            { std::lock_guard<std::mutex> lk(q->m); }
-            q->cv_flusher.notify_one();
-        } else {
-            b->writers.fetch_sub(1, std::memory_order_release);
-        }
-        return 0;
     }
 }
 
@@ -462,9 +618,13 @@ int lcb_hash_queue_flush(lcb_hash_queue_p q) {
 
 int lcb_hash_queue_wait(lcb_hash_queue_p q) {
     if (!q) return EINVAL;
-    const uint64_t target = q->submitted.load(std::memory_order_acquire);
     std::unique_lock<std::mutex> lk(q->m);
-    while (q->completed.load(std::memory_order_acquire) < target) {
+    // Every packet whose submit returned lives in the open slot or an older
+    // one (slots complete in open order); an empty open slot needs no flush.
+    Slot* b = q->open.load(std::memory_order_acquire);
+    const bool empty = st_count(b->state.load(std::memory_order_acquire)) == 0;
+    const uint64_t target = empty ? b->seq - 1 : b->seq;
+    while (q->completed_seq.load(std::memory_order_acquire) < target) {
         q->flush_req.store(true, std::memory_order_release);
         q->cv_flusher.notify_one();
         q->cv_done.wait_for(lk, std::chrono::milliseconds(1));
@@ -482,6 +642,10 @@ int lcb_hash_queue_stats(lcb_hash_queue_p q, lcb_hash_queue_stats_t* st) {
     st->sealed_flush = q->sealed_flush.load();
     st->max_batch_msgs = q->max_batch.load();
     st->submit_waits = q->submit_waits.load();
+    st->flusher_drain_ns = q->drain_ns.load();
+    st->flusher_launch_ns = q->launch_ns.load();
+    st->completer_busy_ns = q->completer_ns.load();
+    st->gpu_wait_ns = q->gpu_wait_ns.load();
     return 0;
 }
 

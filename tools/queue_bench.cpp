@@ -12,7 +12,7 @@
 //
 // usage: queue_bench [--alg 1] [--packets 1048576] [--size 1024] [--threads 8]
 //                    [--flush-us 200] [--batch-msgs 65536] [--batch-bytes 67108864]
-//                    [--slots 4] [--key HEX] [--out FILE]
+//                    [--slots 4] [--align 16] [--key HEX] [--cb 1] [--pool-mib 0] [--out FILE]
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -62,6 +62,9 @@ int main(int argc, char** argv) {
     lcb_hash_queue_settings_def(&cfg);
     cfg.max_batch_bytes = 64u << 20;
     std::string keyhex, out;
+    bool use_cb = true;
+    bool copy_only = false;  // baseline: producers only memcpy into a private arena
+    uint64_t pool_mib = 0;  // 0: every packet distinct (cold source); else cycle a pool this big
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i], v = argv[i + 1];
         if (a == "--alg") alg = atoi(v.c_str());
@@ -75,6 +78,9 @@ int main(int argc, char** argv) {
         else if (a == "--align") cfg.align = (uint32_t)atoi(v.c_str());
         else if (a == "--key") keyhex = v;
         else if (a == "--out") out = v;
+        else if (a == "--cb") use_cb = atoi(v.c_str()) != 0;
+        else if (a == "--pool-mib") pool_mib = strtoull(v.c_str(), nullptr, 0);
+        else if (a == "--copy-only") copy_only = atoi(v.c_str()) != 0;
         else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
     const size_t D = lcb_hash_digest_size(alg);
@@ -84,10 +90,11 @@ int main(int argc, char** argv) {
 
     // Packet pool (the synthetic stream), generated in parallel.
     const uint64_t nbytes = packets * size;
-    std::vector<uint8_t> pool(nbytes + 8);
+    const uint64_t pool_pk = pool_mib ? std::max<uint64_t>(1, (pool_mib << 20) / size) : packets;
+    std::vector<uint8_t> pool(std::min(packets, pool_pk) * size + 8);
     {
         std::vector<std::thread> th;
-        const uint64_t words = (nbytes + 7) / 8;
+        const uint64_t words = (pool.size() - 8 + 7) / 8;
         for (int t = 0; t < threads; ++t)
             th.emplace_back([&, t] {
                 for (uint64_t w = words * t / threads; w < words * (t + 1) / threads; ++w) {
@@ -102,6 +109,29 @@ int main(int argc, char** argv) {
     std::atomic<uint64_t> errors{0};
     g_ctx = Ctx{&t_sub, &t_done, &errors};
 
+    if (copy_only) {
+        // Host-side ceiling for the producers: the same loop, memcpy only.
+        std::vector<uint8_t> arena(nbytes);
+        memset(arena.data(), 0, arena.size());
+        const int64_t c0 = now_ns();
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                const uint64_t lo = packets * t / threads, hi = packets * (t + 1) / threads;
+                for (uint64_t i = lo; i < hi; ++i) {
+                    t_sub[i] = now_ns();
+                    memcpy(&arena[i * size], &pool[(i % pool_pk) * size], size);
+                }
+            });
+        for (auto& x : th) x.join();
+        const double sec = (now_ns() - c0) * 1e-9;
+        printf("{\"copy_only\": 1, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"pool_mib\": %llu, "
+               "\"seconds\": %.4f, \"packets_per_s\": %.0f, \"GiB_s\": %.3f}\n",
+               (unsigned long long)packets, (unsigned long long)size, threads, (unsigned long long)pool_mib, sec,
+               packets / sec, nbytes / sec / (1ull << 30));
+        return 0;
+    }
+
     lcb_hash_queue_p q = nullptr;
     int rc = lcb_hash_queue_create(alg, key.empty() && keyhex.empty() ? nullptr : key.data(), key.size(), &cfg, &q);
     if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
@@ -110,7 +140,7 @@ int main(int argc, char** argv) {
     {
         std::vector<uint8_t> wd(std::min<uint64_t>(packets, 4096) * D);
         for (uint64_t i = 0; i < wd.size() / D; ++i)
-            lcb_hash_queue_submit(q, &pool[i * size], size, &wd[i * D], nullptr, nullptr, 0);
+            lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &wd[i * D], nullptr, nullptr, 0);
         lcb_hash_queue_wait(q);
     }
     lcb_hash_queue_stats_t st0;
@@ -125,8 +155,8 @@ int main(int argc, char** argv) {
                 const uint64_t lo = packets * t / threads, hi = packets * (t + 1) / threads;
                 for (uint64_t i = lo; i < hi; ++i) {
                     t_sub[i] = now_ns();
-                    int r = lcb_hash_queue_submit(q, &pool[i * size], size, &digests[i * D], on_done,
-                                                  (void*)(uintptr_t)i, 0);
+                    int r = lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &digests[i * D],
+                                                  use_cb ? on_done : nullptr, (void*)(uintptr_t)i, 0);
                     if (r) { fail.store(r); return; }
                 }
             });
@@ -143,22 +173,25 @@ int main(int argc, char** argv) {
         return 1;
     }
     std::vector<double> lat(packets);
-    for (uint64_t i = 0; i < packets; ++i) lat[i] = (t_done[i] - t_sub[i]) * 1e-3;
+    for (uint64_t i = 0; i < packets; ++i) lat[i] = use_cb ? (t_done[i] - t_sub[i]) * 1e-3 : 0.0;
     std::sort(lat.begin(), lat.end());
     const double sec = (t1 - t0) * 1e-9;
     printf("{\"alg\": %d, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"flush_usec\": %u, "
-           "\"batch_msgs\": %llu, \"batch_bytes\": %llu, \"slots\": %u, \"seconds\": %.4f, "
+           "\"batch_msgs\": %llu, \"batch_bytes\": %llu, \"slots\": %u, \"pool_mib\": %llu, \"seconds\": %.4f, "
            "\"packets_per_s\": %.0f, \"GiB_s\": %.3f, \"lat_us_p50\": %.1f, \"lat_us_p99\": %.1f, "
            "\"lat_us_max\": %.1f, \"batches\": %llu, \"sealed_full\": %llu, \"sealed_timer\": %llu, "
-           "\"sealed_flush\": %llu, \"submit_waits\": %llu}\n",
+           "\"sealed_flush\": %llu, \"submit_waits\": %llu, \"cb\": %d, \"drain_ms\": %.2f, \"launch_ms\": %.2f, "
+           "\"completer_busy_ms\": %.2f, \"gpu_wait_ms\": %.2f}\n",
            alg, (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
-           (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, sec,
+           (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, (unsigned long long)pool_mib, sec,
            packets / sec, nbytes / sec / (1ull << 30), lat[packets / 2], lat[packets * 99 / 100],
            lat[packets - 1], (unsigned long long)(st.batches - st0.batches),
            (unsigned long long)(st.sealed_full - st0.sealed_full),
            (unsigned long long)(st.sealed_timer - st0.sealed_timer),
            (unsigned long long)(st.sealed_flush - st0.sealed_flush),
-           (unsigned long long)(st.submit_waits - st0.submit_waits));
+           (unsigned long long)(st.submit_waits - st0.submit_waits), (int)use_cb,
+           (st.flusher_drain_ns - st0.flusher_drain_ns) * 1e-6, (st.flusher_launch_ns - st0.flusher_launch_ns) * 1e-6, (st.completer_busy_ns - st0.completer_busy_ns) * 1e-6,
+           (st.gpu_wait_ns - st0.gpu_wait_ns) * 1e-6);
     if (!out.empty()) {
         FILE* f = fopen(out.c_str(), "wb");
         if (!f || fwrite(digests.data(), 1, digests.size(), f) != digests.size()) return 1;
