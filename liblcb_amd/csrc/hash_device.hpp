@@ -54,6 +54,17 @@
 namespace lcbgpu {
 
 // ------------------------------------------------------------ primitives
+// Mark a kernel-argument pointer as global memory.  Pointers read out of the
+// by-value KArgs struct are otherwise generic, and generic loads compile to
+// flat_load, which also counts against lgkmcnt: every wait for an LDS table
+// read would then wait for outstanding HBM loads as well.  The address-space
+// cast lets the compiler's address-space inference turn them into
+// global_load.
+template <class T>
+__device__ __forceinline__ T* gptr(T* p) {
+    return (T*)(__attribute__((address_space(1))) T*)p;
+}
+
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {
     return __builtin_amdgcn_alignbit(x, x, 32u - n);  // v_alignbit_b32
 }
@@ -131,7 +142,7 @@ __device__ __forceinline__ void load_full64(const uint8_t* p, uint32_t w[16]) {
         for (int k = 0; k < 16; ++k) w[k] = q[k];
     } else {
         const uint32_t sh = (uint32_t)(ip & 3u);
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(ip - sh);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
         uint32_t d[17];
 #pragma unroll
         for (int k = 0; k < 17; ++k) d[k] = q[k];
@@ -166,7 +177,7 @@ __device__ __forceinline__ void load_full128(const uint8_t* p, uint32_t w0[16], 
 __device__ __forceinline__ void load_tail64(const uint8_t* p, uint32_t rem, uint32_t w[16]) {
     const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
     const uint32_t sh = (uint32_t)(ip & 3u);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(ip - sh);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
     const uint32_t lim = rem + sh;  // aligned dword j holds a message byte iff 4j < lim
     uint32_t d[17];
 #pragma unroll

@@ -17,12 +17,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/lcb_crc32_gpu.h"
 #include "../../include/lcb_hash_gpu.h"
 #include "lcb_internal.hpp"
 
 namespace lcbgpu {
 
 size_t dsize(int alg) {
+    if (is_crc_alg(alg)) return 4;  // CRC-32: one uint32 per buffer
     static const size_t ds[9] = {0, 16, 20, 28, 32, 48, 64, 32, 64};
     return (alg >= 1 && alg <= 8) ? ds[alg] : 0;
 }
@@ -108,11 +110,12 @@ namespace {
 
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-                 uint32_t fixed_len, uint8_t* digests, hipStream_t s) {
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init = nullptr) {
     KArgs a;
     a.data = data; a.offsets = offsets; a.lengths = lengths; a.order = nullptr;
     a.count = count; a.stride = stride; a.fixed_len = fixed_len; a.digests = digests;
     a.mid = nullptr;
+    a.init = init;
     uint32_t* mid = nullptr;
     uint8_t* dkey = nullptr;
     if (key) {
@@ -137,10 +140,12 @@ struct Stage {
     uint8_t* h_data[2] = {nullptr, nullptr};
     uint64_t* h_off[2] = {nullptr, nullptr};
     uint32_t* h_len[2] = {nullptr, nullptr};
+    uint32_t* h_init[2] = {nullptr, nullptr};   // CRC X_update() values of the chunk
     uint8_t* h_dig[2] = {nullptr, nullptr};
     uint8_t* d_data[2] = {nullptr, nullptr};
     uint64_t* d_off[2] = {nullptr, nullptr};
     uint32_t* d_len[2] = {nullptr, nullptr};
+    uint32_t* d_init[2] = {nullptr, nullptr};
     uint8_t* d_dig[2] = {nullptr, nullptr};
     // pending chunk per buffer (digests to copy out once `done` fires)
     size_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
@@ -151,15 +156,18 @@ struct Stage {
             if (h_data[b]) (void)hipHostFree(h_data[b]);
             if (h_off[b]) (void)hipHostFree(h_off[b]);
             if (h_len[b]) (void)hipHostFree(h_len[b]);
+            if (h_init[b]) (void)hipHostFree(h_init[b]);
             if (h_dig[b]) (void)hipHostFree(h_dig[b]);
             if (d_data[b]) (void)hipFree(d_data[b]);
             if (d_off[b]) (void)hipFree(d_off[b]);
             if (d_len[b]) (void)hipFree(d_len[b]);
+            if (d_init[b]) (void)hipFree(d_init[b]);
             if (d_dig[b]) (void)hipFree(d_dig[b]);
             if (done[b]) (void)hipEventDestroy(done[b]);
             if (st[b]) (void)hipStreamDestroy(st[b]);
             h_data[b] = nullptr; h_off[b] = nullptr; h_len[b] = nullptr; h_dig[b] = nullptr;
             d_data[b] = nullptr; d_off[b] = nullptr; d_len[b] = nullptr; d_dig[b] = nullptr;
+            h_init[b] = nullptr; d_init[b] = nullptr;
             done[b] = nullptr; st[b] = nullptr;
         }
         cap = mcap = 0;
@@ -178,10 +186,12 @@ struct Stage {
             LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_data[b]), nb, hipHostMallocDefault));
             LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_off[b]), nm * 8, hipHostMallocDefault));
             LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_len[b]), nm * 4, hipHostMallocDefault));
+            LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_init[b]), nm * 4, hipHostMallocDefault));
             LCB_TRY(hipHostMalloc(reinterpret_cast<void**>(&h_dig[b]), nm * 64, hipHostMallocDefault));
             LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_data[b]), nb));
             LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_off[b]), nm * 8));
             LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_len[b]), nm * 4));
+            LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_init[b]), nm * 4));
             LCB_TRY(hipMalloc(reinterpret_cast<void**>(&d_dig[b]), nm * 64));
         }
         cap = nb;
@@ -232,7 +242,7 @@ void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
 
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-               uint32_t fixed_len, uint8_t* digests) {
+               uint32_t fixed_len, uint8_t* digests, const uint32_t* init = nullptr) {
     int dev = 0;
     LCB_TRY(hipGetDevice(&dev));
     const size_t D = dsize(alg);
@@ -302,7 +312,13 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
         KArgs a;
         a.order = nullptr; a.count = n; a.digests = S.d_dig[b]; a.mid = mid;
         bool ok = true;
-        if (direct) {
+        if (init) {  // CRC X_update() values of this chunk
+            memcpy(S.h_init[b], init + i, n * 4);
+            ok = hipMemcpyAsync(S.d_init[b], S.h_init[b], n * 4, hipMemcpyHostToDevice, s) == hipSuccess;
+            a.init = S.d_init[b];
+        }
+        if (!ok) {
+        } else if (direct) {
             ok = hipMemcpyAsync(S.d_data[b], data + base, span ? span : 1, hipMemcpyHostToDevice, s) == hipSuccess;
             if (fixed) {
                 a.data = S.d_data[b]; a.offsets = nullptr; a.lengths = nullptr;
@@ -390,7 +406,7 @@ const char* lcb_hash_strerror(int error) {
 int lcb_hash_batch(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                    const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                    uint32_t fixed_len, uint8_t* digests, uint32_t flags, void* stream) {
-    if (dsize(alg) == 0) return EINVAL;
+    if (alg < LCB_HASH_MD5 || alg > LCB_HASH_GOST512) return EINVAL;
     if (flags & ~LCB_HASH_F_DEVICE) return EINVAL;
     if (count == 0) return 0;
     if (!data || !digests) return EINVAL;
@@ -497,6 +513,50 @@ int lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t* dev_out, size
 int lcb_hash_gpu_gost_table(uint64_t* out) {
     if (!out) return EINVAL;
     gost_table_host(out);
+    return 0;
+}
+
+}  // extern "C"
+
+// ================================================================ CRC-32
+extern "C" {
+
+int lcb_crc32_batch(int variant, const uint32_t* init, const uint8_t* data, const uint64_t* offsets,
+                    const uint32_t* lengths, size_t count, uint64_t stride, uint32_t fixed_len,
+                    uint32_t* crcs, uint32_t flags, void* stream) {
+    if (variant < LCB_CRC32A || variant > LCB_CRC32Q) return EINVAL;
+    if (flags & ~LCB_HASH_F_DEVICE) return EINVAL;
+    if (count == 0) return 0;
+    if (!data || !crcs || (reinterpret_cast<uintptr_t>(crcs) & 3u)) return EINVAL;
+    if (int rc = ensure_init()) return rc;
+    const int alg = kCrcAlgBase + variant;
+    uint8_t* out = reinterpret_cast<uint8_t*>(crcs);
+    if (flags & LCB_HASH_F_DEVICE)
+        return batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, out,
+                            reinterpret_cast<hipStream_t>(stream), init);
+    return batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, out, init);
+}
+
+#define LCB_CRC_ENTRY(name, id)                                                                       \
+    int name##_batch(const uint32_t* init, const uint8_t* data, const uint64_t* offsets,              \
+                     const uint32_t* lengths, size_t count, uint64_t stride, uint32_t fixed_len,      \
+                     uint32_t* crcs, uint32_t flags, void* stream) {                                  \
+        return lcb_crc32_batch(id, init, data, offsets, lengths, count, stride, fixed_len, crcs,       \
+                               flags, stream);                                                        \
+    }
+LCB_CRC_ENTRY(crc32a, LCB_CRC32A)
+LCB_CRC_ENTRY(crc32cksum, LCB_CRC32CKSUM)
+LCB_CRC_ENTRY(crc32mpeg2, LCB_CRC32MPEG2)
+LCB_CRC_ENTRY(crc32b, LCB_CRC32B)
+LCB_CRC_ENTRY(crc32jamcrc, LCB_CRC32JAMCRC)
+LCB_CRC_ENTRY(crc32c, LCB_CRC32C)
+LCB_CRC_ENTRY(crc32d, LCB_CRC32D)
+LCB_CRC_ENTRY(crc32q, LCB_CRC32Q)
+#undef LCB_CRC_ENTRY
+
+int lcb_crc32_gpu_tables(int variant, uint32_t* out) {
+    if (variant < LCB_CRC32A || variant > LCB_CRC32Q || !out) return EINVAL;
+    crc_table_host(variant, out);
     return 0;
 }
 

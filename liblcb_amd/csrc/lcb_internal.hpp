@@ -14,8 +14,9 @@ struct KArgs {
     uint64_t count;
     uint64_t stride;
     uint32_t fixed_len;
-    uint8_t* digests;          // packed count x D
+    uint8_t* digests;          // packed count x D (CRC: count x uint32)
     const uint32_t* mid;       // HMAC mid-states (nullptr: plain digest)
+    const uint32_t* init = nullptr;  // CRC: per-buffer X_update() value (nullptr: one-shot X())
 };
 
 // Words reserved per HMAC mid-state (GOST needs 34: h, N, Sigma).
@@ -31,7 +32,14 @@ constexpr int kLenClasses = 128;
 // Ragged batches at least this large are bucketed by length first.
 constexpr uint64_t kBucketMinCount = 4096;
 
+// CRC-32 variants travel through the batch machinery as alg ids
+// kCrcAlgBase + variant (variant ids of include/lcb_crc32_gpu.h).
+constexpr int kCrcAlgBase = 100;
+inline bool is_crc_alg(int alg) { return alg > kCrcAlgBase && alg <= kCrcAlgBase + 8; }
+
 void launch_batch(int alg, const KArgs& a, hipStream_t s);
+void launch_crc(int variant, const KArgs& a, hipStream_t s);
+void crc_table_host(int variant, uint32_t* out);
 void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, uint32_t* order,
                       hipStream_t s);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,

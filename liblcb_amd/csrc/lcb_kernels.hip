@@ -14,9 +14,9 @@ namespace lcbgpu {
 __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.count) return false;
-    idx = a.order ? (uint64_t)a.order[i] : i;
-    msg = a.data + (a.offsets ? a.offsets[idx] : idx * a.stride);
-    len = a.lengths ? (uint64_t)a.lengths[idx] : (uint64_t)a.fixed_len;
+    idx = a.order ? (uint64_t)gptr(a.order)[i] : i;
+    msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
+    len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
     return true;
 }
 
@@ -367,6 +367,9 @@ void launch_batch(int alg, const KArgs& a, hipStream_t s) {
     case 6: launch_md<Sha512<false>>(a, hmac, s); break;
     case 7: launch_gost<true>(a, hmac, s); break;
     case 8: launch_gost<false>(a, hmac, s); break;
+    default:
+        if (is_crc_alg(alg)) launch_crc(alg - kCrcAlgBase, a, s);
+        break;
     }
 }
 

@@ -9,14 +9,16 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDR = os.path.join(ROOT, "include", "lcb_hash_gpu.h")
+HDRS = [os.path.join(ROOT, "include", h) for h in ("lcb_hash_gpu.h", "lcb_hash_queue.h", "lcb_crc32_gpu.h")]
 SO = os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so")
 
 
 def declared_functions():
-    src = open(HDR).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b([a-z_0-9]+)\s*\(", src)) - {"defined"})
+    names = set()
+    for h in HDRS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b([a-z_0-9]+)\(", src)) - {"defined", "sizeof"}
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -27,13 +29,13 @@ def L():
 
 def test_exports_every_declared_symbol(L):
     names = declared_functions()
-    assert len(names) == 16, names
+    assert len(names) == 16 + 8 + 10, names
     out = subprocess.check_output(["nm", "-D", "--defined-only", SO]).decode()
     exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
     missing = [n for n in names if n not in exported]
     assert not missing, missing
-    from liblcb_amd._lib import SIGNATURES
-    assert sorted(n for n, _, _ in SIGNATURES) == names
+    from liblcb_amd._lib import CRC_SIGNATURES, QUEUE_SIGNATURES, SIGNATURES
+    assert sorted(n for n, _, _ in SIGNATURES + QUEUE_SIGNATURES + CRC_SIGNATURES) == names
 
 
 def test_info_calls(L):
@@ -97,3 +99,50 @@ def test_gost_table_matches_reference(L):
         assert np.array_equal(t, Ref().gost_ax())
     # Independently: LPS of 0 through the table equals the first column.
     assert t[0] == t[256 * 0 + 0] and len(set(t[:256].tolist())) == 256
+
+
+def test_crc32_argument_errors(L):
+    buf = np.zeros(64, np.uint8)
+    out = np.zeros(4, np.uint32)
+    assert L.lcb_crc32_batch(0, None, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL
+    assert L.lcb_crc32_batch(9, None, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL
+    assert L.lcb_crc32_batch(1, None, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data + 1, 0, None) == errno.EINVAL
+    assert L.lcb_crc32_batch(1, None, None, None, None, 1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL
+    assert L.lcb_crc32_batch(1, None, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 4, None) == errno.EINVAL
+    assert L.crc32c_batch(None, buf.ctypes.data, None, None, 0, 0, 8, out.ctypes.data, 0, None) == 0
+    # the digest entry point does not take CRC ids
+    assert L.lcb_hash_batch(101, None, 0, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL
+
+
+def test_crc32_fails_loudly_without_gpu(L):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    import liblcb_amd.crc32 as c
+    with pytest.raises(liblcb_amd_error()):
+        c.crc32c_batch(np.zeros(64, np.uint8), count=1, fixed_len=8)
+
+
+def liblcb_amd_error():
+    import liblcb_amd
+    return liblcb_amd.LcbHashError
+
+
+def test_crc32_tables_match_reference(L):
+    """Table 0 of every variant == the reference's crc32_tbl256_*; table k is
+    table k-1 advanced by one zero byte."""
+    from oracle.pyoracle import Oracle, Ref
+    ref = Ref() if Ref.available() else Oracle()
+    for v in range(1, 9):
+        t = np.zeros(8 * 256, np.uint32)
+        assert L.lcb_crc32_gpu_tables(v, t.ctypes.data) == 0
+        t = t.reshape(8, 256)
+        assert np.array_equal(t[0], ref.crc32_table(v)), v
+        refl = v in (4, 5, 6, 7)
+        for k in range(1, 8):
+            p = t[k - 1].astype(np.uint64)
+            if refl:
+                want = (p >> 8) ^ t[0][(p & 255).astype(np.int64)]
+            else:
+                want = ((p << 8) & 0xffffffff) ^ t[0][(p >> 24).astype(np.int64)]
+            assert np.array_equal(t[k], want.astype(np.uint32)), (v, k)
