@@ -23,6 +23,7 @@ import ctypes
 import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -149,7 +150,26 @@ def cpu_baseline(alg, count, threads):
         t = time.perf_counter() - t0
         res["port"] = (count * MSG_LEN / t / 2**30, t, d, 1)
     best = max(res, key=lambda k: res[k][0])
-    return best, res
+    # Single-thread rate of the best build on a bounded sample (~1 s).
+    one = None
+    path = {"reference": REF_SO, "reference-simd": REF_SIMD_SO}.get(best)
+    if path:
+        r = Ref(path)
+        n1 = min(count, 1 << 18)
+        t0 = time.perf_counter()
+        r.batch_fixed_mt(alg, data[:n1 * MSG_LEN], n1, MSG_LEN, MSG_LEN, threads=1)
+        one = n1 * MSG_LEN / (time.perf_counter() - t0) / 2**30
+    return best, res, one
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
@@ -185,6 +205,60 @@ def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
     del data, dig
     torch.cuda.empty_cache()
     return res
+
+
+def bench_crc(data, count, steps):
+    """CRC-32 family (include/math/crc32.h) over the same
+    1M x 1 KiB device-resident bytes: per-variant kernel time (HIP events,
+    after 3 warm launches) and HBM fraction of the algorithmic bytes
+    (count x (1024 + 4))."""
+    from liblcb_amd.crc32 import CRC_NAMES
+    out_t = torch.empty(count, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    res = {}
+    for v, name in CRC_NAMES.items():
+        def launch():
+            check(lib().lcb_crc32_batch(v, None, data.data_ptr(), None, None, count, MSG_LEN, MSG_LEN,
+                                        out_t.data_ptr(), F_DEVICE, stream.cuda_stream))
+        for _ in range(3):
+            launch()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for e0, e1 in ev:
+            e0.record(stream)
+            launch()
+            e1.record(stream)
+        torch.cuda.synchronize()
+        km = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+        res[name] = {"GiB_s": round(count * MSG_LEN / (km * 1e-3) / 2**30, 2), "kernel_ms": round(km, 4),
+                     "hbm_frac": round(count * (MSG_LEN + 4) / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    del out_t
+    return res
+
+
+def bench_ingest(alg_id, packets=1 << 21, threads=8):
+    """Asynchronous ingestion queue (include/lcb_hash_queue.h, SURVEY.md 8f
+    row 2): `threads` native producer threads submit 1 KiB packets from host
+    memory; packets/s and submit->callback latency, plus the same producers
+    doing only the memcpy into host memory (the host-side ceiling).  Runs
+    tools/queue_bench as a child process."""
+    exe = os.path.join(ROOT, "tools", "queue_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/queue_bench not built"}
+    base = [exe, "--alg", str(alg_id), "--packets", str(packets), "--size", str(MSG_LEN),
+            "--threads", str(threads)]
+    res = {}
+    for key, extra in (("queue", []), ("copy_only", ["--copy-only", "1"])):
+        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": r.stderr.strip()[-300:]}
+        res[key] = json.loads(r.stdout.strip().splitlines()[-1])
+    q = res["queue"]
+    return {"packets_per_s": q["packets_per_s"], "GiB_s": q["GiB_s"], "lat_us_p50": q["lat_us_p50"],
+            "lat_us_p99": q["lat_us_p99"], "batches": q["batches"], "threads": threads,
+            "packet_bytes": MSG_LEN, "settings": "64K packets / 64 MiB / 200 us / 4 slots",
+            "copy_only_GiB_s": res["copy_only"]["GiB_s"],
+            "path": "producer memcpy into pinned lease -> H2D -> kernel -> D2H -> per-packet callback"}
 
 
 def main():
@@ -247,6 +321,8 @@ def main():
             del dg
         out["per_alg"] = per
         out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
+        out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
+        out["ingest"] = bench_ingest(alg)
         # End-to-end host path on the same bytes (lcb_hash_batch host mode):
         # pinned input is DMA'd straight from the caller's buffer, pageable
         # input is gathered into pinned staging first; 64 MiB chunks on two
@@ -270,7 +346,7 @@ def main():
 
     if rank == 0 and world == 1 and not a.no_cpu:
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        best, res = cpu_baseline(alg, count, threads)
+        best, res, one = cpu_baseline(alg, count, threads)
         gbs, tcpu, dcpu, reps = res[best]
         gpu_dig = digests.cpu().numpy()
         out["cpu_baseline"] = {
@@ -279,6 +355,10 @@ def main():
             "build": best, "sample": "the full workload (%d x %d B, %s) hashed %d times on %d threads, "
             "one contiguous shard per thread, %.1f s wall" % (count, MSG_LEN, a.alg, reps, threads, tcpu),
             "all": {k: round(v[0], 3) for k, v in res.items()},
+            "one_thread": round(one, 3) if one else None,
+            "cpu_model": cpu_model(),
+            "build_flags": {"reference": "gcc -O2 -fPIC, #undef __SSE2__ (as tests/hash/main.c:36)",
+                            "reference-simd": "gcc -O2 -fPIC -msse4.1 -mssse3 -msha -mavx2 (cpuid dispatch)"},
             "seconds": round(tcpu, 3)}
         out.setdefault("verify", {})["gpu_equals_cpu_reference"] = bool(np.array_equal(gpu_dig, dcpu))
         out["verify"]["digest_of_digests"] = hashlib.sha256(gpu_dig.tobytes()).hexdigest()
