@@ -79,6 +79,22 @@ int or_crc32_batch(int variant, const uint32_t *init, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lengths, size_t count,
     uint64_t stride, uint32_t fixed_len, uint32_t *crcs);
 
+/*
+ * ChaCha of include/crypto/cipher/chacha.h (oracle/chacha_oracle.c).
+ * key_size: 256 or 32 -> 256-bit key, anything else -> 128-bit (chacha.h:289).
+ * counter8 / iv8 / iv24 may be NULL (zero).  src NULL -> keystream.
+ */
+void or_hchacha(const uint8_t *key, size_t key_size, const uint8_t *iv16, size_t rounds, uint8_t *out32);
+void or_chacha(const uint8_t *key, size_t key_size, const uint8_t *counter8, const uint8_t *iv8,
+    size_t rounds, const uint8_t *src, size_t n, uint8_t *dst);
+void or_xchacha(const uint8_t *key, size_t key_size, const uint8_t *counter8, const uint8_t *iv24,
+    size_t rounds, const uint8_t *src, size_t n, uint8_t *dst);
+/* Buffer i (same layout in src and dst): counters + 8*i, ivs + (x ? 24 : 8)*i. */
+int or_chacha_batch(const uint8_t *key, size_t key_size, size_t rounds, int x,
+    const uint8_t *counters, const uint8_t *ivs, const uint8_t *src, uint8_t *dst,
+    const uint64_t *offsets, const uint32_t *lengths, size_t count, uint64_t stride,
+    uint32_t fixed_len);
+
 /* Synthetic-input generator: byte b of the stream is byte
  * (b & 7) of splitmix64_mix(seed ^ (b >> 3)).  Writes n bytes starting at
  * stream byte position `start`. */

@@ -121,7 +121,46 @@ class _Crc:
         return out
 
 
-class Oracle(_Batch, _Crc):
+_CHA_ARGS = [_c.c_void_p, _c.c_size_t, _c.c_size_t, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+             _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_uint64, _c.c_uint32]
+
+
+class _Cha:
+    fn_cha = None
+
+    def chacha_batch(self, key, key_size, rounds, src, offsets=None, lengths=None, count=None,
+                     stride=0, fixed_len=0, counters=None, ivs=None, x=False, nbytes=None):
+        """dst with buffer i = chacha()/xchacha() of buffer i (chacha.h:650-679);
+        src None -> keystream into a zeroed buffer of nbytes."""
+        key = np.frombuffer(bytes(key), np.uint8)
+        kbuf = np.zeros(max(32, key.size), np.uint8)
+        kbuf[:key.size] = key
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if count is None:
+            count = len(lengths) if lengths is not None else len(offsets)
+        if src is not None:
+            src = np.ascontiguousarray(src, dtype=np.uint8)
+            dst = np.zeros(max(src.size, 1), np.uint8)
+        else:
+            dst = np.zeros(max(int(nbytes), 1), np.uint8)
+        if counters is not None:
+            counters = np.ascontiguousarray(counters, dtype=np.uint8)
+        if ivs is not None:
+            ivs = np.ascontiguousarray(ivs, dtype=np.uint8)
+        rc = self.fn_cha(kbuf.ctypes.data, key_size, rounds, 1 if x else 0,
+                         counters.ctypes.data if counters is not None else None,
+                         ivs.ctypes.data if ivs is not None else None,
+                         src.ctypes.data if src is not None and src.size else None, dst.ctypes.data,
+                         offsets.ctypes.data if offsets is not None else None,
+                         lengths.ctypes.data if lengths is not None else None, count, stride, fixed_len)
+        assert rc == 0, rc
+        return dst
+
+
+class Oracle(_Batch, _Crc, _Cha):
     """The C restatement."""
 
     def __init__(self, path=ORACLE_SO):
@@ -133,6 +172,8 @@ class Oracle(_Batch, _Crc):
         self.lib.or_init.argtypes = [_c.c_void_p, _c.c_int]
         self.lib.or_update.argtypes = [_c.c_void_p, _c.c_char_p, _c.c_size_t]
         self.lib.or_final.argtypes = [_c.c_void_p, _c.c_char_p]
+        self.lib.or_chacha_batch.argtypes = _CHA_ARGS
+        self.fn_cha = self.lib.or_chacha_batch
         self.lib.or_crc32_batch.argtypes = _CRC_ARGS
         self.fn_crc = self.lib.or_crc32_batch
         self.lib.or_crc32_table.restype = _c.c_uint32
@@ -155,7 +196,7 @@ class Oracle(_Batch, _Crc):
         return out.raw[:DSIZE[alg]]
 
 
-class Ref(_Batch, _Crc):
+class Ref(_Batch, _Crc, _Cha):
     """The reference's own code (compiled from /root/reference into _ref/)."""
 
     def __init__(self, path=REF_SO):
@@ -163,6 +204,8 @@ class Ref(_Batch, _Crc):
         self.lib.ref_batch.argtypes = _ARGS
         self.fn_batch = self.lib.ref_batch
         self.lib.ref_gost_ax.argtypes = [_c.c_void_p]
+        self.lib.ref_chacha_batch.argtypes = _CHA_ARGS
+        self.fn_cha = self.lib.ref_chacha_batch
         self.lib.ref_crc32_batch.argtypes = _CRC_ARGS
         self.fn_crc = self.lib.ref_crc32_batch
         self.lib.ref_crc32_table.argtypes = [_c.c_int, _c.c_void_p]
@@ -174,6 +217,32 @@ class Ref(_Batch, _Crc):
 
     def crc32_self_test(self):
         return self.lib.ref_crc32_self_test()
+
+    def chacha_self_test(self):
+        return self.lib.ref_chacha_self_test()
+
+    def chacha_kats(self):
+        """chacha_self_test's vector table, decoded by the reference's own
+        import helpers (chacha.h:968-1040)."""
+        out = []
+        i = 0
+        while True:
+            key = _c.create_string_buffer(32)
+            cnt = _c.create_string_buffer(8)
+            iv = _c.create_string_buffer(8)
+            exp = _c.create_string_buffer(2048)
+            plain = _c.create_string_buffer(2048)
+            ks, rounds, size = _c.c_size_t(), _c.c_size_t(), _c.c_size_t()
+            hc, hi, hp = _c.c_int(), _c.c_int(), _c.c_int()
+            if self.lib.ref_chacha_kat(_c.c_size_t(i), key, _c.byref(ks), cnt, _c.byref(hc), iv, _c.byref(hi),
+                                       _c.byref(rounds), _c.byref(size), exp, plain, _c.byref(hp)) != 0:
+                return out
+            out.append({"key": key.raw.hex(), "key_size": ks.value,
+                        "counter": cnt.raw.hex() if hc.value else None,
+                        "iv": iv.raw.hex() if hi.value else None, "rounds": rounds.value,
+                        "plain": plain.raw[:size.value].hex() if hp.value else None,
+                        "output": exp.raw[:size.value].hex()})
+            i += 1
 
     @staticmethod
     def available(path=REF_SO):

@@ -40,6 +40,9 @@
 #endif
 #define CRC32_SELF_TEST 1
 #include "math/crc32.h"
+#include <errno.h>
+#define CHACHA_SELF_TEST 1
+#include "crypto/cipher/chacha.h"
 
 enum { A_MD5 = 1, A_SHA1, A_SHA224, A_SHA256, A_SHA384, A_SHA512, A_GOST256, A_GOST512 };
 
@@ -204,5 +207,69 @@ ref_crc32_table(int v, uint32_t *out) {
 	default: return -1;
 	}
 	memcpy(out, t, 256 * sizeof(uint32_t));
+	return 0;
+}
+
+/* ---------------------------------------------------------------- ChaCha
+ * include/crypto/cipher/chacha.h one-shot chacha() / xchacha() per buffer. */
+int
+ref_chacha_self_test(void) {
+	return chacha_self_test();	/* chacha.h:1061-1160 */
+}
+
+int
+ref_chacha_batch(const uint8_t *key, size_t key_size, size_t rounds, int x,
+    const uint8_t *counters, const uint8_t *ivs, const uint8_t *src, uint8_t *dst,
+    const uint64_t *offsets, const uint32_t *lengths, size_t count, uint64_t stride,
+    uint32_t fixed_len) {
+	size_t i, ivlen = (x ? 24 : 8);
+
+	for (i = 0; i < count; i ++) {
+		uint64_t o = (offsets ? offsets[i] : (uint64_t)i * stride);
+		size_t n = (lengths ? lengths[i] : fixed_len);
+		const uint8_t *c = (counters ? counters + 8 * i : NULL);
+		const uint8_t *v = (ivs ? ivs + ivlen * i : NULL);
+		if (x)
+			xchacha(key, key_size, c, v, rounds, (src ? src + o : NULL), n, dst + o);
+		else
+			chacha(key, key_size, c, v, rounds, (src ? src + o : NULL), n, dst + o);
+	}
+	return 0;
+}
+
+/* The self test's first table (chacha.h:709-...), decoded exactly as
+ * chacha_self_test does: vector i -> key (32), count (8, NULL -> flag 0),
+ * iv (8), rounds, data size, expected output, plaintext (NULL -> keystream
+ * test).  Returns -1 past the end. */
+int
+ref_chacha_kat(size_t i, uint8_t *key, size_t *key_size, uint8_t *count, int *has_count,
+    uint8_t *iv, int *has_iv, size_t *rounds, size_t *data_size, uint8_t *expected,
+    uint8_t *plain, int *has_plain) {
+	size_t n;
+
+	for (n = 0; 0 != chacha_tst1v[n].rounds; n ++)
+		;
+	if (i >= n)
+		return -1;
+	memset(key, 0, CHACHA_KEY_256_LEN);
+	chacha_import_le_hex(key, CHACHA_KEY_256_LEN, chacha_tst1v[i].key, chacha_tst1v[i].key_size);
+	*key_size = chacha_tst1v[i].key_size / 2;
+	*has_count = (NULL != chacha_tst1v[i].count);
+	memset(count, 0, 8);
+	if (*has_count)
+		chacha_import_be_hex(count, 8, chacha_tst1v[i].count, 16);
+	*has_iv = (NULL != chacha_tst1v[i].iv);
+	memset(iv, 0, 8);
+	if (*has_iv)
+		chacha_import_le_hex(iv, 8, chacha_tst1v[i].iv, 16);
+	*rounds = chacha_tst1v[i].rounds;
+	*data_size = chacha_tst1v[i].data_size / 2;
+	chacha_import_le_hex(expected, CHACHA_TEST_LEN, chacha_tst1v[i].encrypted,
+	    chacha_tst1v[i].data_size);
+	*has_plain = (NULL != chacha_tst1v[i].plain);
+	memset(plain, 0, CHACHA_TEST_LEN);
+	if (*has_plain)
+		chacha_import_le_hex(plain, CHACHA_TEST_LEN, chacha_tst1v[i].plain,
+		    chacha_tst1v[i].data_size);
 	return 0;
 }
