@@ -3,13 +3,14 @@
 The product is the C-ABI library liblcb_hash_gpu.so (include/lcb_hash_gpu.h,
 HIP kernels in csrc/).  This package is its host-side Python mirror of the
 reference's one-shot API (liblcb_amd.hash), the CRC-32 family of
-include/math/crc32.h (liblcb_amd.crc32) and the asynchronous packet
-ingestion queue (liblcb_amd.queue).
+include/math/crc32.h (liblcb_amd.crc32), the ChaCha / XChaCha cipher of
+include/crypto/cipher/chacha.h (liblcb_amd.chacha) and the asynchronous
+packet ingestion queue (liblcb_amd.queue).
 """
 from ._lib import (ALG_IDS, ALG_NAMES, BLOCK_SIZE, DIGEST_SIZE, GOST256, GOST512, MD5, SHA1,
                    SHA224, SHA256, SHA384, SHA512, LcbHashError, lib)
 from .hash import *  # noqa: F401,F403
-from . import crc32, queue  # noqa: F401,E402  (CRC-32 family, ingestion queue)
+from . import chacha, crc32, queue  # noqa: F401,E402  (cipher, CRC-32 family, ingestion queue)
 
 __all__ = ["ALG_IDS", "ALG_NAMES", "BLOCK_SIZE", "DIGEST_SIZE", "MD5", "SHA1", "SHA224",
            "SHA256", "SHA384", "SHA512", "GOST256", "GOST512", "LcbHashError", "lib"]

@@ -69,6 +69,13 @@ CRC_SIGNATURES = [("lcb_crc32_batch", ctypes.c_int, [ctypes.c_int] + _CRC),
     ("crc32a", "crc32cksum", "crc32mpeg2", "crc32b", "crc32jamcrc", "crc32c", "crc32d", "crc32q")]
 
 
+_CHA = [c_vp, c_sz, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_u32, c_vp]
+# every symbol include/lcb_chacha_gpu.h declares
+CHACHA_SIGNATURES = [("lcb_chacha_batch", ctypes.c_int, [ctypes.c_int] + _CHA),
+                     ("chacha_batch", ctypes.c_int, _CHA),
+                     ("xchacha_batch", ctypes.c_int, _CHA)]
+
+
 class QueueSettings(ctypes.Structure):
     """lcb_hash_queue_settings_t (include/lcb_hash_queue.h)."""
     _fields_ = [("max_batch_msgs", c_sz), ("max_batch_bytes", c_sz), ("flush_usec", c_u32),
@@ -119,7 +126,7 @@ def lib():
             raise RuntimeError("%s is missing: build it with `python -c 'import __graft_entry__ as g; "
                                "g.build()'` (or `make -C liblcb_amd`)" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
-        for name, res, args in SIGNATURES + QUEUE_SIGNATURES + CRC_SIGNATURES:
+        for name, res, args in SIGNATURES + QUEUE_SIGNATURES + CRC_SIGNATURES + CHACHA_SIGNATURES:
             if os.environ.get("LCB_HASH_GPU_LIB") and not hasattr(L, name):
                 continue  # an older experiment build: bind what it has
             fn = getattr(L, name)

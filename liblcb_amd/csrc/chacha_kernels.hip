@@ -1,0 +1,364 @@
+// chacha_kernels.hip — batched ChaCha / XChaCha (include/lcb_chacha_gpu.h)
+// for gfx950.
+//
+// Unlike the digests, ChaCha is a counter-mode keystream: every 64-byte
+// block of every buffer is independent (chacha.h:423-446 — the state only
+// differs in the 64-bit block counter).  So the unit of work is a BLOCK, not
+// a buffer, and the kernel is laid out for coalesced HBM streams:
+//
+//  * FOUR LANES PER BLOCK (a "quad").  Lane q of a quad holds column q of the
+//    4x4 state (words q, 4+q, 8+q, 12+q).  The column round is then four
+//    independent lane-local quarter rounds; the diagonal round needs rows 1-3
+//    rotated by 1/2/3 lanes, which is a DPP quad_perm on the operand (folded
+//    into the consuming v_add/v_xor by the compiler: no extra instruction).
+//    This is the SIMD-register formulation of ChaCha mapped onto wave64 DPP.
+//  * After the rounds a two-stage DPP transpose gives lane q the keystream
+//    words 4q..4q+3 = bytes [16q, 16q+16) of its block, so one wavefront
+//    instruction loads / stores 16 blocks x 64 B = 1 KiB contiguous
+//    (16 B per lane, the coalescing sweet spot) when the buffers are dense.
+//  * Each lane carries B blocks (16 quads x B blocks = a wave TILE of
+//    consecutive blocks) for instruction-level parallelism; the grid is
+//    persistent (grid-stride over tiles), its exit condition is the block
+//    total every wave reads, so every wave terminates.
+//
+// Block -> buffer: fixed-length batches divide (bpb blocks per buffer);
+// ragged batches binary-search an exclusive prefix of blocks per buffer
+// built on the device by chacha_scan_* (no host round trip).
+//
+// Buffers at any byte alignment: 16-B aligned full slices use dwordx4; other
+// slices use aligned dword slots with v_alignbyte funnel shifts and byte
+// stores only at the buffer edges.  No byte outside a described buffer is
+// read past its containing dword, and none is written.
+#include <hip/hip_runtime.h>
+
+#include "hash_device.hpp"
+#include "lcb_internal.hpp"
+
+#ifndef LCB_CHA_B
+#define LCB_CHA_B 2
+#endif
+
+namespace lcbgpu {
+
+// DPP quad_perm controls: lane q reads lane p_q of its quad.
+constexpr int kQpRot1 = 0x39;   // [1,2,3,0]  lane q <- q+1
+constexpr int kQpRot2 = 0x4E;   // [2,3,0,1]  lane q <- q+2
+constexpr int kQpRot3 = 0x93;   // [3,0,1,2]  lane q <- q+3
+constexpr int kQpSwp1 = 0xB1;   // [1,0,3,2]  lane q <- q^1
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+
+// chacha.h:125-130
+__device__ __forceinline__ void cha_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    a += b; d = rotl32(d ^ a, 16);
+    c += d; b = rotl32(b ^ c, 12);
+    a += b; d = rotl32(d ^ a, 8);
+    c += d; b = rotl32(b ^ c, 7);
+}
+
+// One double round (chacha.h:132-141) of the quad formulation: lane q holds
+// column q as (a, b, c, d) = rows 0..3.
+__device__ __forceinline__ void cha_dround_quad(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    cha_qr(a, b, c, d);                                            // columns
+    b = qperm<kQpRot1>(b); c = qperm<kQpRot2>(c); d = qperm<kQpRot3>(d);
+    cha_qr(a, b, c, d);                                            // diagonals
+    b = qperm<kQpRot3>(b); c = qperm<kQpRot2>(c); d = qperm<kQpRot1>(d);
+}
+
+// Whole-state double round in one lane (hchacha prep).
+__device__ __forceinline__ void cha_dround_full(uint32_t* x) {
+    cha_qr(x[0], x[4], x[8], x[12]); cha_qr(x[1], x[5], x[9], x[13]);
+    cha_qr(x[2], x[6], x[10], x[14]); cha_qr(x[3], x[7], x[11], x[15]);
+    cha_qr(x[0], x[5], x[10], x[15]); cha_qr(x[1], x[6], x[11], x[12]);
+    cha_qr(x[2], x[7], x[8], x[13]); cha_qr(x[3], x[4], x[9], x[14]);
+}
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+    return q == 0 ? v0 : (q == 1 ? v1 : (q == 2 ? v2 : v3));
+}
+
+// ----------------------------------------------------------- hchacha prep
+// xchacha: subkey_i = hchacha(key, iv_i[0:16]) (chacha.h:361-401), one lane
+// per buffer; the block kernel then runs chacha with that 256-bit key.
+__global__ __launch_bounds__(256) void hchacha_kernel(ChaArgs a, uint32_t* subkeys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.count) return;
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = a.hcst[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[4 + k] = a.key[k];
+    const uint32_t* iv = a.ivs ? gptr(a.ivs) + i * a.iv_words : nullptr;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[12 + k] = iv ? iv[k] : 0u;
+    for (uint32_t r = 0; r < a.dr; ++r) cha_dround_full(x);
+    uint32_t* o = gptr(subkeys) + i * 8;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        o[k] = x[k];
+        o[4 + k] = x[12 + k];
+    }
+}
+
+// ------------------------------------------------- ragged: block prefix
+// blk_start[i] = sum_{k<i} ceil(len_k / 64), blk_start[count] = total.
+// Three passes of 1024 buffers per workgroup (4 per thread).
+constexpr int kScanPer = 1024;
+
+__device__ __forceinline__ uint64_t blocks_of(uint32_t len) { return ((uint64_t)len + 63u) >> 6; }
+
+// Inclusive scan of one value per thread over the 256-thread workgroup.
+__device__ __forceinline__ uint64_t wg_inclusive_scan(uint64_t v, uint64_t* sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint64_t add = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
+        __syncthreads();
+        v += add;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void chacha_scan_reduce(const uint32_t* lengths, uint64_t count,
+                                                          uint64_t* parts) {
+    __shared__ uint64_t sh[256];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanPer + threadIdx.x * 4u;
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + k < count) s += blocks_of(gptr(lengths)[base + k]);
+    const uint64_t inc = wg_inclusive_scan(s, sh);
+    if (threadIdx.x == 255) gptr(parts)[blockIdx.x] = inc;
+}
+
+// One workgroup: exclusive scan of the per-workgroup sums, in place.
+__global__ __launch_bounds__(256) void chacha_scan_parts(uint64_t* parts, uint64_t nparts) {
+    __shared__ uint64_t sh[256];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nparts; b += 256) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < nparts ? gptr(parts)[i] : 0u;
+        const uint64_t inc = wg_inclusive_scan(v, sh);
+        if (i < nparts) gptr(parts)[i] = carry + inc - v;
+        carry += sh[255];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void chacha_scan_final(const uint32_t* lengths, uint64_t count,
+                                                         const uint64_t* parts, uint64_t* blk_start) {
+    __shared__ uint64_t sh[256];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanPer + threadIdx.x * 4u;
+    uint64_t b[4], s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        b[k] = base + k < count ? blocks_of(gptr(lengths)[base + k]) : 0u;
+        s += b[k];
+    }
+    const uint64_t inc = wg_inclusive_scan(s, sh);
+    uint64_t run = gptr(parts)[blockIdx.x] + inc - s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (base + k < count) gptr(blk_start)[base + k] = run;
+        run += b[k];
+        if (base + k + 1 == count) gptr(blk_start)[count] = run;
+    }
+}
+
+// ------------------------------------------------------------ block kernel
+// Which buffer holds global block g, and g's block index inside it.
+__device__ __forceinline__ void cha_locate(const ChaArgs& a, uint64_t g, uint64_t total, uint64_t& buf,
+                                           uint64_t& jb) {
+    if (a.lengths == nullptr) {
+        if (total <= 0xffffffffull) {  // wave-uniform: 32-bit division suffices
+            const uint32_t b = (uint32_t)g / a.bpb;
+            buf = b;
+            jb = (uint32_t)g - b * a.bpb;
+        } else {
+            buf = g / a.bpb;
+            jb = g - buf * a.bpb;
+        }
+        return;
+    }
+    // Largest i with blk_start[i] <= g (blk_start[count] = total > g; a
+    // zero-length buffer shares its start with the next one and is skipped).
+    const uint64_t* bs = gptr(a.blk_start);
+    uint64_t lo = 0, hi = a.count;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bs[mid] <= g) lo = mid; else hi = mid;
+    }
+    buf = lo;
+    jb = g - bs[lo];
+}
+
+// XOR keystream slice K (bytes [0,16) of the lane's slice) into dst[0, n)
+// (src NULL: store K itself), at any alignment, touching only those bytes.
+__device__ __forceinline__ void cha_store_slice(uint8_t* d, const uint8_t* s, uint32_t n, const uint32_t K[4]) {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(d), as = reinterpret_cast<uintptr_t>(s);
+    if (n == 16 && ((ad | as) & 15u) == 0) {
+        uint4 v = s ? *reinterpret_cast<const uint4*>(s) : make_uint4(0, 0, 0, 0);
+        v.x ^= K[0]; v.y ^= K[1]; v.z ^= K[2]; v.w ^= K[3];
+        *reinterpret_cast<uint4*>(d) = v;
+        return;
+    }
+    if (s && ((ad ^ as) & 3u)) {  // src and dst misaligned differently: bytes
+        for (uint32_t b = 0; b < n; ++b) d[b] = s[b] ^ (uint8_t)(K[b >> 2] >> (8u * (b & 3u)));
+        return;
+    }
+    // Dword slots k = 0..4 of the aligned window starting at d - sh.  Slot k
+    // holds slice bytes [4k - sh, 4k - sh + 4).
+    const uint32_t sh = (uint32_t)(ad & 3u);
+    uint8_t* db = d - sh;
+    const uint8_t* sb = s ? s - sh : nullptr;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int first = 4 * k - (int)sh;
+        const int lo = first < 0 ? 0 : first;
+        const int hi = (first + 4) < (int)n ? first + 4 : (int)n;
+        if (lo >= hi) continue;
+        const uint32_t kh = k < 4 ? K[k] : 0u, kl = k > 0 ? K[k - 1] : 0u;
+        const uint32_t kw = sh ? __builtin_amdgcn_alignbyte(kh, kl, 4u - sh) : kh;
+        const uint32_t v = (sb ? *reinterpret_cast<const uint32_t*>(sb + 4 * k) : 0u) ^ kw;
+        if (lo == first && hi == first + 4) {
+            *reinterpret_cast<uint32_t*>(db + 4 * k) = v;
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (first + b >= lo && first + b < hi) db[4 * k + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}
+
+template <int DR, int B>
+__global__ __launch_bounds__(256) void chacha_kernel(ChaArgs a) {
+    const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, quad = lane >> 2;
+    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t total = a.lengths ? gptr(a.blk_start)[a.count] : a.total_blocks;
+    const uint32_t dr = a.dr;
+    // Column q, rows 0-2 (constants and key), shared by every block unless
+    // the key is per buffer (xchacha subkeys).
+    const uint32_t r0 = sel4(q, a.cst[0], a.cst[1], a.cst[2], a.cst[3]);
+    const uint32_t k1 = sel4(q, a.key[0], a.key[1], a.key[2], a.key[3]);
+    const uint32_t k2 = sel4(q, a.key[4], a.key[5], a.key[6], a.key[7]);
+    // All-ones where this lane keeps its own odd (keep1) / upper-half (keep2)
+    // registers in the two transpose stages.
+    const uint32_t keep1 = (q & 1u) ? 0xffffffffu : 0u, keep2 = (q & 2u) ? 0xffffffffu : 0u;
+    constexpr uint64_t kTile = 16u * B;
+    for (uint64_t t = wave0; t * kTile < total; t += nwaves) {
+        uint32_t x0[B], x1[B], x2[B], x3[B], o1[B], o2[B], o3[B], n[B];
+        uint64_t boff[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            uint64_t g = t * kTile + (uint64_t)j * 16u + quad;
+            const bool live = g < total;
+            if (!live) g = total - 1;  // compute on a valid block, store nothing
+            uint64_t buf, jb;
+            cha_locate(a, g, total, buf, jb);
+            const uint64_t off = a.offsets ? gptr(a.offsets)[buf] : buf * a.stride;
+            const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[buf] : (uint64_t)a.fixed_len;
+            const uint64_t p = jb * 64u + 16u * q;
+            n[j] = (live && len > p) ? (uint32_t)(len - p < 16u ? len - p : 16u) : 0u;
+            boff[j] = off + p;
+            uint32_t w3;
+            if (q < 2) {  // 64-bit block counter + j (chacha.h:319-327, 440-444)
+                uint64_t ctr = 0;
+                if (a.counters) {
+                    const uint32_t* c = gptr(a.counters) + 2 * buf;
+                    ctr = (uint64_t)c[0] | ((uint64_t)c[1] << 32);
+                }
+                ctr += jb;
+                w3 = q ? (uint32_t)(ctr >> 32) : (uint32_t)ctr;
+            } else {  // IV words (chacha.h:344-355)
+                w3 = a.ivs ? gptr(a.ivs)[buf * a.iv_words + a.iv_at + (q - 2)] : 0u;
+            }
+            uint32_t kk1 = k1, kk2 = k2;
+            if (a.subkeys) {
+                const uint32_t* sk = gptr(a.subkeys) + 8 * buf;
+                kk1 = sk[q];
+                kk2 = sk[4 + q];
+            }
+            x0[j] = r0; x1[j] = o1[j] = kk1; x2[j] = o2[j] = kk2; x3[j] = o3[j] = w3;
+        }
+        // Fully unrolled for the standard round counts so the un-rotation
+        // DPP of one double round folds into the next one's first ops.
+        if (DR) {
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)DR; ++r) {
+#pragma unroll
+                for (int j = 0; j < B; ++j) cha_dround_quad(x0[j], x1[j], x2[j], x3[j]);
+            }
+        } else {
+            for (uint32_t r = 0; r < dr; ++r) {
+#pragma unroll
+                for (int j = 0; j < B; ++j) cha_dround_quad(x0[j], x1[j], x2[j], x3[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            // Feed-forward (chacha.h:143-161): lane q holds words 4r + q.
+            uint32_t m[4] = {x0[j] + r0, x1[j] + o1[j], x2[j] + o2[j], x3[j] + o3[j]};
+            // Transpose the quad's 4x4 so lane q holds words 4q + r.
+            // The selects are bitwise (v_bitop3) on purpose: written as `?:`
+            // the compiler turns them into exec-masked branches and sinks the
+            // DPP read into them, where the partner lane is masked off.
+            uint32_t t1[4], K[4], sw[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sw[r] = qperm<kQpSwp1>(m[r ^ 1]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t1[r] = ch3((r & 1) ? keep1 : ~keep1, m[r], sw[r]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sw[r] = qperm<kQpRot2>(t1[r ^ 2]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) K[r] = ch3((r & 2) ? keep2 : ~keep2, t1[r], sw[r]);
+            if (n[j]) {
+                uint8_t* d = gptr(a.dst) + boff[j];
+                const uint8_t* s = a.src ? gptr(a.src) + boff[j] : nullptr;
+                cha_store_slice(d, s, n[j], K);
+            }
+        }
+    }
+}
+
+template <int DR>
+static void launch_cha_dr(const ChaArgs& a, unsigned grid, hipStream_t s) {
+    hipLaunchKernelGGL((chacha_kernel<DR, LCB_CHA_B>), dim3(grid), dim3(256), 0, s, a);
+}
+
+void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t* blk_start,
+                   uint32_t* subkeys, hipStream_t s) {
+    ChaArgs k = a;
+    if (a.lengths) {
+        const unsigned nb = (unsigned)((a.count + kScanPer - 1) / kScanPer);
+        hipLaunchKernelGGL(chacha_scan_reduce, dim3(nb), dim3(256), 0, s, a.lengths, a.count, parts);
+        hipLaunchKernelGGL(chacha_scan_parts, dim3(1), dim3(256), 0, s, parts, nparts);
+        hipLaunchKernelGGL(chacha_scan_final, dim3(nb), dim3(256), 0, s, a.lengths, a.count,
+                           (const uint64_t*)parts, blk_start);
+        k.blk_start = blk_start;
+    }
+    if (subkeys) {
+        hipLaunchKernelGGL(hchacha_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, s, a,
+                           subkeys);
+        k.subkeys = subkeys;
+    }
+    // Persistent grid: enough workgroups to fill 256 CUs several times over,
+    // fewer when the (known) fixed-layout total needs fewer tiles.
+    constexpr uint64_t kTile = 16u * LCB_CHA_B, kMaxGrid = 4096;
+    uint64_t grid = kMaxGrid;
+    if (!a.lengths) grid = std::min<uint64_t>(kMaxGrid, (a.total_blocks + 4 * kTile - 1) / (4 * kTile));
+    if (grid == 0) grid = 1;
+    switch (a.dr) {
+    case 4: launch_cha_dr<4>(k, (unsigned)grid, s); break;     // ChaCha8
+    case 6: launch_cha_dr<6>(k, (unsigned)grid, s); break;     // ChaCha12
+    case 10: launch_cha_dr<10>(k, (unsigned)grid, s); break;   // ChaCha20
+    default: launch_cha_dr<0>(k, (unsigned)grid, s); break;
+    }
+}
+
+}  // namespace lcbgpu

@@ -102,6 +102,37 @@ int ensure_init() {
     return g_init_rc;
 }
 
+// True when `p` is page-locked host memory the DMA engines can read directly
+// (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory()).
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+// memcpy of many (dst, src, n) pieces, split over up to 8 host threads when
+// the chunk is large (the single-thread staging copy was the host-path bound).
+void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
+    const size_t nt = bytes >= (8u << 20) ? std::min<size_t>(8, pieces.size()) : 1;
+    if (nt <= 1) {
+        for (const Piece& p : pieces) memcpy(p.dst, p.src, p.n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (pieces.size() + nt - 1) / nt;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t lo = t * per, hi = std::min(pieces.size(), lo + per);
+        if (lo >= hi) break;
+        th.emplace_back([&pieces, lo, hi] {
+            for (size_t k = lo; k < hi; ++k) memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
 }  // namespace lcbgpu
 
 using namespace lcbgpu;
@@ -203,42 +234,6 @@ struct Stage {
 thread_local Stage g_stage;
 constexpr size_t kChunkBytes = 64ull << 20;   // 64 MiB per in-flight chunk
 constexpr size_t kChunkMsgs = 1u << 18;       // 256 K messages per chunk
-
-// True when `p` is page-locked host memory the DMA engines can read directly
-// (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory()).
-bool is_pinned(const void* p) {
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-        (void)hipGetLastError();  // pageable memory reports an error: clear it
-        return false;
-    }
-    return attr.type == hipMemoryTypeHost;
-}
-
-// memcpy of many (dst, src, n) pieces, split over up to 8 host threads when
-// the chunk is large (the single-thread staging copy was the host-path bound).
-struct Piece {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-};
-void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
-    const size_t nt = bytes >= (8u << 20) ? std::min<size_t>(8, pieces.size()) : 1;
-    if (nt <= 1) {
-        for (const Piece& p : pieces) memcpy(p.dst, p.src, p.n);
-        return;
-    }
-    std::vector<std::thread> th;
-    const size_t per = (pieces.size() + nt - 1) / nt;
-    for (size_t t = 0; t < nt; ++t) {
-        const size_t lo = t * per, hi = std::min(pieces.size(), lo + per);
-        if (lo >= hi) break;
-        th.emplace_back([&pieces, lo, hi] {
-            for (size_t k = lo; k < hi; ++k) memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
-        });
-    }
-    for (auto& x : th) x.join();
-}
 
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,

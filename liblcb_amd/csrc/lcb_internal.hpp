@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace lcbgpu {
 
 // Device-side description of one batch (see include/lcb_hash_gpu.h).
@@ -37,7 +39,31 @@ constexpr uint64_t kBucketMinCount = 4096;
 constexpr int kCrcAlgBase = 100;
 inline bool is_crc_alg(int alg) { return alg > kCrcAlgBase && alg <= kCrcAlgBase + 8; }
 
+// Device-side description of one ChaCha batch (see include/lcb_chacha_gpu.h).
+struct ChaArgs {
+    const uint8_t* src = nullptr;         // nullptr: write the keystream itself
+    uint8_t* dst = nullptr;
+    const uint64_t* offsets = nullptr;    // nullptr: i * stride
+    const uint32_t* lengths = nullptr;    // nullptr: fixed_len
+    const uint64_t* blk_start = nullptr;  // ragged: exclusive block prefix (count + 1)
+    const uint32_t* counters = nullptr;   // 2 LE words per buffer, nullptr: 0
+    const uint32_t* ivs = nullptr;        // iv_words per buffer, nullptr: 0
+    const uint32_t* subkeys = nullptr;    // xchacha: 8 words per buffer
+    uint64_t count = 0, stride = 0;
+    uint64_t total_blocks = 0;            // fixed layout: count * bpb
+    uint32_t fixed_len = 0, bpb = 1;
+    uint32_t iv_words = 2, iv_at = 0;     // chacha 2,0; xchacha 6,4
+    uint32_t dr = 10;                     // double rounds = ceil(rounds / 2)
+    uint32_t key[8] = {};                 // state words 4..11
+    uint32_t cst[4] = {};                 // state words 0..3 of the block function
+    uint32_t hcst[4] = {};                // state words 0..3 of hchacha (xchacha)
+};
+
 void launch_batch(int alg, const KArgs& a, hipStream_t s);
+// ChaCha: ragged scan (parts: (count+1023)/1024 words, blk_start: count+1),
+// xchacha subkey prep (subkeys: 8 words per buffer), then the block kernel.
+void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t* blk_start,
+                   uint32_t* subkeys, hipStream_t s);
 void launch_crc(int variant, const KArgs& a, hipStream_t s);
 void crc_table_host(int variant, uint32_t* out);
 void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, uint32_t* order,
@@ -58,5 +84,14 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
                uint8_t** dkey_out);
 // Batch kernel launch, bucketing a large ragged batch by length first.
 int launch_ordered(int alg, KArgs a, hipStream_t s);
+
+// Host-memory helpers shared by the host-mode pipelines.
+bool is_pinned(const void* p);  // page-locked (DMA-able) host memory
+struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+void parallel_copy(const std::vector<Piece>& pieces, size_t bytes);  // up to 8 threads
 
 }  // namespace lcbgpu

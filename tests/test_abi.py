@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDRS = [os.path.join(ROOT, "include", h) for h in ("lcb_hash_gpu.h", "lcb_hash_queue.h", "lcb_crc32_gpu.h")]
+HDRS = [os.path.join(ROOT, "include", h) for h in ("lcb_hash_gpu.h", "lcb_hash_queue.h", "lcb_crc32_gpu.h", "lcb_chacha_gpu.h")]
 SO = os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so")
 
 
@@ -29,13 +29,14 @@ def L():
 
 def test_exports_every_declared_symbol(L):
     names = declared_functions()
-    assert len(names) == 16 + 8 + 10, names
+    assert len(names) == 16 + 8 + 10 + 3, names
     out = subprocess.check_output(["nm", "-D", "--defined-only", SO]).decode()
     exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
     missing = [n for n in names if n not in exported]
     assert not missing, missing
-    from liblcb_amd._lib import CRC_SIGNATURES, QUEUE_SIGNATURES, SIGNATURES
-    assert sorted(n for n, _, _ in SIGNATURES + QUEUE_SIGNATURES + CRC_SIGNATURES) == names
+    from liblcb_amd._lib import CHACHA_SIGNATURES, CRC_SIGNATURES, QUEUE_SIGNATURES, SIGNATURES
+    sigs = SIGNATURES + QUEUE_SIGNATURES + CRC_SIGNATURES + CHACHA_SIGNATURES
+    assert sorted(n for n, _, _ in sigs) == names
 
 
 def test_info_calls(L):
@@ -146,3 +147,29 @@ def test_crc32_tables_match_reference(L):
             else:
                 want = ((p << 8) & 0xffffffff) ^ t[0][(p >> 24).astype(np.int64)]
             assert np.array_equal(t[k], want.astype(np.uint32)), (v, k)
+
+
+def test_chacha_argument_errors(L):
+    key = np.zeros(32, np.uint8)
+    buf = np.zeros(64, np.uint8)
+    k, b = key.ctypes.data, buf.ctypes.data
+    # null key / dst, unknown flags, unbounded rounds -> EINVAL before touching HIP
+    assert L.lcb_chacha_batch(0, None, 32, None, None, 20, b, b, None, None, 1, 0, 8, 0, None) == errno.EINVAL
+    assert L.lcb_chacha_batch(0, k, 32, None, None, 20, b, None, None, None, 1, 0, 8, 0, None) == errno.EINVAL
+    assert L.lcb_chacha_batch(0, k, 32, None, None, 20, b, b, None, None, 1, 0, 8, 0x10, None) == errno.EINVAL
+    assert L.chacha_batch(k, 32, None, None, 1 << 20, b, b, None, None, 1, 0, 8, 0, None) == errno.EINVAL
+    # empty batch is a no-op
+    assert L.xchacha_batch(k, 32, None, None, 20, b, b, None, None, 0, 0, 8, 0, None) == 0
+
+
+def test_chacha_fails_loudly_without_gpu(L):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    key = np.zeros(32, np.uint8)
+    buf = np.zeros(64, np.uint8)
+    assert L.chacha_batch(key.ctypes.data, 32, None, None, 20, buf.ctypes.data, buf.ctypes.data, None, None,
+                          1, 0, 64, 0, None) == errno.ENODEV
+    import liblcb_amd.chacha as c
+    with pytest.raises(liblcb_amd_error()):
+        c.chacha_batch(bytes(32), np.zeros(64, np.uint8), count=1, fixed_len=64)
