@@ -4,26 +4,35 @@
 // Unlike the digests, ChaCha is a counter-mode keystream: every 64-byte
 // block of every buffer is independent (chacha.h:423-446 — the state only
 // differs in the 64-bit block counter).  So the unit of work is a BLOCK, not
-// a buffer, and the kernel is laid out for coalesced HBM streams:
+// a buffer.
 //
-//  * FOUR LANES PER BLOCK (a "quad").  Lane q of a quad holds column q of the
-//    4x4 state (words q, 4+q, 8+q, 12+q).  The column round is then four
-//    independent lane-local quarter rounds; the diagonal round needs rows 1-3
-//    rotated by 1/2/3 lanes, which is a DPP quad_perm on the operand (folded
-//    into the consuming v_add/v_xor by the compiler: no extra instruction).
-//    This is the SIMD-register formulation of ChaCha mapped onto wave64 DPP.
-//  * After the rounds a two-stage DPP transpose gives lane q the keystream
-//    words 4q..4q+3 = bytes [16q, 16q+16) of its block, so one wavefront
-//    instruction loads / stores 16 blocks x 64 B = 1 KiB contiguous
-//    (16 B per lane, the coalescing sweet spot) when the buffers are dense.
-//  * Each lane carries B blocks (16 quads x B blocks = a wave TILE of
-//    consecutive blocks) for instruction-level parallelism; the grid is
-//    persistent (grid-stride over tiles), its exit condition is the block
-//    total every wave reads, so every wave terminates.
+// chacha_lane_kernel (the product): ONE LANE PER BLOCK, the whole 4x4 state
+// in 16 VGPRs, 80 quarter rounds with 4-way ILP inside the lane and no
+// cross-lane traffic — the minimum VALU work per block.  Register-only
+// throughput (tools/cha_core.hip on MI355X) is ~0.41-0.45 ms of ChaCha20 per
+// GiB whatever the layout, so ChaCha20 is VALU-bound and ChaCha8/12 are
+// HBM-bound.  For the memory side, a dense batch of whole aligned blocks
+// (the bench layout) takes the STREAM path: the wave's 64 blocks = 4 KiB
+// are read and written by four coalesced 1 KiB instructions (16 B per
+// lane), and the keystream is redistributed lane-per-block -> lane-per-16-B
+// through a bank-conflict-free swizzled LDS slab.  Other layouts (ragged,
+// misaligned, partial blocks) go through per-lane 16-B / dword-slot /
+// byte paths.  The grid is persistent (grid-stride over 64-block wave
+// tiles), sized to the resident workgroup count, and every wave's exit
+// condition is the block total it reads.
 //
-// Block -> buffer: fixed-length batches divide (bpb blocks per buffer);
-// ragged batches binary-search an exclusive prefix of blocks per buffer
-// built on the device by chacha_scan_* (no host round trip).
+// chacha_kernel (compiled out, LCB_CHA_QUAD=1): FOUR LANES PER BLOCK, lane q
+// holding column q; the diagonal round rotates rows 1-3 by DPP quad_perm
+// (folded into the consuming v_add/v_xor by the compiler) and a two-stage
+// DPP transpose gives lane q bytes [16q, 16q+16) for coalesced stores.
+// Measured: same register-only VALU rate as the lane layout, but more
+// per-block overhead (every lane of the quad redoes the block bookkeeping);
+// 0.59-0.67 ms ChaCha20 vs 0.55 for the lane kernel.  Kept for A/B.
+//
+// Block -> buffer: fixed-length batches divide once per wave and then step
+// (bpb blocks per buffer); ragged batches search an exclusive prefix of
+// blocks per buffer built on the device by chacha_scan_* (a 64-ary wave
+// search for the tile's first buffer, then a short per-lane gallop).
 //
 // Buffers at any byte alignment: 16-B aligned full slices use dwordx4; other
 // slices use aligned dword slots with v_alignbyte funnel shifts and byte
@@ -35,7 +44,10 @@
 #include "lcb_internal.hpp"
 
 #ifndef LCB_CHA_B
-#define LCB_CHA_B 2
+#define LCB_CHA_B 1
+#endif
+#ifndef LCB_CHA_PREFETCH_MAXDR
+#define LCB_CHA_PREFETCH_MAXDR 6
 #endif
 
 namespace lcbgpu {
@@ -171,30 +183,46 @@ __global__ __launch_bounds__(256) void chacha_scan_final(const uint32_t* lengths
 }
 
 // ------------------------------------------------------------ block kernel
-// Which buffer holds global block g, and g's block index inside it.
-__device__ __forceinline__ void cha_locate(const ChaArgs& a, uint64_t g, uint64_t total, uint64_t& buf,
-                                           uint64_t& jb) {
-    if (a.lengths == nullptr) {
-        if (total <= 0xffffffffull) {  // wave-uniform: 32-bit division suffices
-            const uint32_t b = (uint32_t)g / a.bpb;
-            buf = b;
-            jb = (uint32_t)g - b * a.bpb;
-        } else {
-            buf = g / a.bpb;
-            jb = g - buf * a.bpb;
-        }
-        return;
+// Ragged batches: largest i with blk_start[i] <= g0 for a wave-uniform g0
+// (blk_start[count] = total > g0; a zero-length buffer shares its start with
+// the next one and is skipped).  64-ary search: each step the wave loads 64
+// evenly spaced prefix entries of the live interval and a ballot picks the
+// sub-interval, so 1M buffers take 4 vector loads instead of 20 dependent
+// ones.
+__device__ __forceinline__ uint64_t cha_wave_search(const uint64_t* bs, uint64_t count, uint64_t g0,
+                                                    uint32_t lane) {
+    uint64_t lo = 0, hi = count;
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t idx = lo + (uint64_t)lane * step;
+        const bool le = idx < hi && bs[idx] <= g0;  // a prefix of the lanes (bs is sorted)
+        const uint32_t k = (uint32_t)__popcll(__ballot(le)) - 1u;  // lane 0 always qualifies
+        lo = lo + (uint64_t)k * step;
+        const uint64_t nh = lo + step;
+        hi = nh < hi ? nh : hi;
     }
-    // Largest i with blk_start[i] <= g (blk_start[count] = total > g; a
-    // zero-length buffer shares its start with the next one and is skipped).
-    const uint64_t* bs = gptr(a.blk_start);
-    uint64_t lo = 0, hi = a.count;
+    return lo;
+}
+
+// Per lane: the buffer holding block g >= blk_start[lo], galloping forward
+// from the tile's first buffer then bisecting (blocks of one tile are
+// consecutive, so the distance is small unless many buffers are empty).
+__device__ __forceinline__ uint64_t cha_lane_search(const uint64_t* bs, uint64_t count, uint64_t lo, uint64_t g) {
+    uint64_t hi = count;
+    for (uint64_t s = 1;; s <<= 1) {
+        const uint64_t c = lo + s;
+        if (c >= count) break;
+        if (bs[c] > g) {
+            hi = c;
+            break;
+        }
+        lo = c;
+    }
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
         if (bs[mid] <= g) lo = mid; else hi = mid;
     }
-    buf = lo;
-    jb = g - bs[lo];
+    return lo;
 }
 
 // XOR keystream slice K (bytes [0,16) of the lane's slice) into dst[0, n)
@@ -238,9 +266,17 @@ __device__ __forceinline__ void cha_store_slice(uint8_t* d, const uint8_t* s, ui
 template <int DR, int B>
 __global__ __launch_bounds__(256) void chacha_kernel(ChaArgs a) {
     const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, quad = lane >> 2;
-    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const uint64_t total = a.lengths ? gptr(a.blk_start)[a.count] : a.total_blocks;
+    // Wave-uniform tile bookkeeping (readfirstlane: the compiler cannot see
+    // that threadIdx.x >> 6 is uniform, and would keep it all in VGPRs).
+    const uint64_t wave0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                           (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t total = a.total_blocks;
+    if (a.lengths) {
+        const uint64_t tv = gptr(a.blk_start)[a.count];
+        total = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tv);
+    }
     const uint32_t dr = a.dr;
     // Column q, rows 0-2 (constants and key), shared by every block unless
     // the key is per buffer (xchacha subkeys).
@@ -251,16 +287,47 @@ __global__ __launch_bounds__(256) void chacha_kernel(ChaArgs a) {
     // registers in the two transpose stages.
     const uint32_t keep1 = (q & 1u) ? 0xffffffffu : 0u, keep2 = (q & 2u) ? 0xffffffffu : 0u;
     constexpr uint64_t kTile = 16u * B;
+    // Fixed layout: (buf0, jb0) of the tile's first block, advanced by the
+    // grid stride without dividing again.
+    const uint64_t bpb = a.bpb;
+    const uint64_t gstep = nwaves * kTile;
+    uint64_t buf0 = 0, jb0 = 0, sdiv = 0, smod = 0;
+    if (!a.lengths) {
+        buf0 = (wave0 * kTile) / bpb;
+        jb0 = wave0 * kTile - buf0 * bpb;
+        sdiv = gstep / bpb;
+        smod = gstep - sdiv * bpb;
+    }
     for (uint64_t t = wave0; t * kTile < total; t += nwaves) {
+        const uint64_t g0 = t * kTile;
+        if (a.lengths) buf0 = cha_wave_search(gptr(a.blk_start), a.count, g0, lane);
         uint32_t x0[B], x1[B], x2[B], x3[B], o1[B], o2[B], o3[B], n[B];
         uint64_t boff[B];
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            uint64_t g = t * kTile + (uint64_t)j * 16u + quad;
+            const uint32_t d = (uint32_t)j * 16u + quad;
+            uint64_t g = g0 + d;
             const bool live = g < total;
             if (!live) g = total - 1;  // compute on a valid block, store nothing
             uint64_t buf, jb;
-            cha_locate(a, g, total, buf, jb);
+            if (a.lengths) {
+                buf = cha_lane_search(gptr(a.blk_start), a.count, buf0, g);
+                jb = g - gptr(a.blk_start)[buf];
+            } else if (bpb >= kTile) {  // at most one buffer boundary inside the tile
+                jb = jb0 + d;
+                buf = buf0;
+                if (jb >= bpb) {
+                    jb -= bpb;
+                    ++buf;
+                }
+                if (buf >= a.count) buf = a.count - 1;  // dead lane past the end: stores nothing
+            } else {  // short buffers: small 32-bit division
+                const uint32_t r = (uint32_t)jb0 + d;
+                const uint32_t k = r / (uint32_t)bpb;
+                buf = buf0 + k;
+                jb = r - k * (uint32_t)bpb;
+                if (buf >= a.count) buf = a.count - 1;
+            }
             const uint64_t off = a.offsets ? gptr(a.offsets)[buf] : buf * a.stride;
             const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[buf] : (uint64_t)a.fixed_len;
             const uint64_t p = jb * 64u + 16u * q;
@@ -323,12 +390,226 @@ __global__ __launch_bounds__(256) void chacha_kernel(ChaArgs a) {
                 cha_store_slice(d, s, n[j], K);
             }
         }
+        if (!a.lengths) {
+            buf0 += sdiv;
+            jb0 += smod;
+            if (jb0 >= bpb) {
+                jb0 -= bpb;
+                ++buf0;
+            }
+        }
     }
 }
 
+// ------------------------------------------------- lane-per-block kernel
+// One lane per 64-byte block: the whole 4x4 state in 16 VGPRs, no
+// cross-lane traffic.  Per block this is the minimum VALU work (80 quarter
+// rounds, 4-way ILP inside the lane) — the quad/DPP kernel above spends
+// ~30-50 % more VALU per block on DPP-carrying ops and its transpose.  The
+// src block is loaded before the rounds so its latency hides behind them.
 template <int DR>
-static void launch_cha_dr(const ChaArgs& a, unsigned grid, hipStream_t s) {
-    hipLaunchKernelGGL((chacha_kernel<DR, LCB_CHA_B>), dim3(grid), dim3(256), 0, s, a);
+__global__ __launch_bounds__(256) void chacha_lane_kernel(ChaArgs a) {
+    __shared__ uint4 cha_lds[4][256];  // per wave: 64 blocks x 4 slices of keystream
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                           (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t total = a.total_blocks;
+    if (a.lengths) {
+        const uint64_t tv = gptr(a.blk_start)[a.count];
+        total = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tv);
+    }
+    constexpr uint64_t kTile = 64;
+    const uint64_t bpb = a.bpb;
+    const uint64_t gstep = nwaves * kTile;
+    uint64_t buf0 = 0, jb0 = 0, sdiv = 0, smod = 0;
+    if (!a.lengths) {
+        buf0 = (wave0 * kTile) / bpb;
+        jb0 = wave0 * kTile - buf0 * bpb;
+        sdiv = gstep / bpb;
+        smod = gstep - sdiv * bpb;
+    }
+    for (uint64_t t = wave0; t * kTile < total; t += nwaves) {
+        const uint64_t g0 = t * kTile;
+        uint64_t g = g0 + lane, buf, jb;
+        const bool live = g < total;
+        if (!live) g = total - 1;
+        if (a.lengths) {
+            buf0 = cha_wave_search(gptr(a.blk_start), a.count, g0, lane);
+            buf = cha_lane_search(gptr(a.blk_start), a.count, buf0, g);
+            jb = g - gptr(a.blk_start)[buf];
+        } else if (bpb >= kTile) {
+            jb = jb0 + lane;
+            buf = buf0;
+            if (jb >= bpb) {
+                jb -= bpb;
+                ++buf;
+            }
+            if (buf >= a.count) buf = a.count - 1;
+        } else {
+            const uint32_t r = (uint32_t)jb0 + lane;
+            const uint32_t k = r / (uint32_t)bpb;
+            buf = buf0 + k;
+            jb = r - k * (uint32_t)bpb;
+            if (buf >= a.count) buf = a.count - 1;
+        }
+        const uint64_t off = a.offsets ? gptr(a.offsets)[buf] : buf * a.stride;
+        const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[buf] : (uint64_t)a.fixed_len;
+        const uint64_t p = jb * 64u;
+        const uint32_t n = (live && len > p) ? (uint32_t)(len - p < 64u ? len - p : 64u) : 0u;
+        uint8_t* dp = gptr(a.dst) + off + p;
+        const uint8_t* sp = a.src ? gptr(a.src) + off + p : nullptr;
+        // Stream tile (wave-uniform): the batch is one dense 16-B aligned run
+        // of whole blocks (block g at byte 64 g) and this tile is full, so
+        // the wave's 4 KiB are read and written by 4 coalesced 1 KiB
+        // instructions (lane l <-> bytes 1024 k + 16 l); the keystream is
+        // redistributed through LDS (below).
+        const bool stream = a.stream && g0 + kTile <= total;
+        const bool fast = !stream && n == 64 &&
+                          ((reinterpret_cast<uintptr_t>(dp) | reinterpret_cast<uintptr_t>(sp)) & 15u) == 0;
+        // Prefetch the source before the rounds when they are short (the
+        // memory-bound ChaCha8/12); for long rounds load after them and keep
+        // the 16 VGPRs for occupancy instead.
+        constexpr bool kPrefetch = DR != 0 && DR <= LCB_CHA_PREFETCH_MAXDR;
+        uint4 in[4] = {};
+        if (kPrefetch && stream && a.src) {
+            const uint4* sb = reinterpret_cast<const uint4*>(gptr(a.src) + g0 * 64u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) in[k] = sb[64 * k + lane];
+        } else if (kPrefetch && fast && sp) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) in[k] = reinterpret_cast<const uint4*>(sp)[k];
+        }
+        // State (chacha.h:69-75): constants, key, 64-bit counter + jb, IV.
+        uint32_t s[16], x[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = a.cst[k];
+        if (a.subkeys) {
+            const uint4* sk = reinterpret_cast<const uint4*>(gptr(a.subkeys) + 8 * buf);
+            const uint4 u = sk[0], v = sk[1];
+            s[4] = u.x; s[5] = u.y; s[6] = u.z; s[7] = u.w;
+            s[8] = v.x; s[9] = v.y; s[10] = v.z; s[11] = v.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s[4 + k] = a.key[k];
+        }
+        uint64_t ctr = jb;
+        if (a.counters) {
+            const uint32_t* c = gptr(a.counters) + 2 * buf;
+            ctr += (uint64_t)c[0] | ((uint64_t)c[1] << 32);
+        }
+        s[12] = (uint32_t)ctr;
+        s[13] = (uint32_t)(ctr >> 32);
+        if (a.ivs) {
+            const uint32_t* iv = gptr(a.ivs) + buf * a.iv_words + a.iv_at;
+            s[14] = iv[0];
+            s[15] = iv[1];
+        } else {
+            s[14] = s[15] = 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = s[k];
+        if (DR) {
+#pragma unroll
+            for (int r = 0; r < DR; ++r) cha_dround_full(x);
+        } else {
+            for (uint32_t r = 0; r < a.dr; ++r) cha_dround_full(x);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] += s[k];  // chacha.h:143-161
+        if (stream) {
+            // Keystream block `lane`, slice i -> LDS slot 4 lane + (i ^ h),
+            // h = (lane >> 1) & 3: conflict-free for the 8-lane groups of
+            // ds_write_b128 and for the 16-lane groups of ds_read_b128 below
+            // (MI355X_MICROARCH.md LDS lane groups).  Wave-private region.
+            uint4* L = cha_lds[threadIdx.x >> 6];
+            const uint32_t h = (lane >> 1) & 3u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                L[4 * lane + ((uint32_t)i ^ h)] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (!kPrefetch && a.src) {
+                const uint4* sb = reinterpret_cast<const uint4*>(gptr(a.src) + g0 * 64u);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) in[k] = sb[64 * k + lane];
+            }
+            uint4* db = reinterpret_cast<uint4*>(gptr(a.dst) + g0 * 64u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t b = 16u * k + (lane >> 2), sl = lane & 3u;
+                const uint4 kv = L[4 * b + (sl ^ ((b >> 1) & 3u))];
+                uint4 v = in[k];
+                v.x ^= kv.x; v.y ^= kv.y; v.z ^= kv.z; v.w ^= kv.w;
+                db[64 * k + lane] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else if (fast) {
+            if (!kPrefetch && sp) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) in[k] = reinterpret_cast<const uint4*>(sp)[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint4 v = in[k];
+                v.x ^= x[4 * k]; v.y ^= x[4 * k + 1]; v.z ^= x[4 * k + 2]; v.w ^= x[4 * k + 3];
+                reinterpret_cast<uint4*>(dp)[k] = v;
+            }
+        } else if (n) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int nk = (int)n - 16 * k;
+                if (nk > 0) cha_store_slice(dp + 16 * k, sp ? sp + 16 * k : nullptr, nk < 16 ? nk : 16, &x[4 * k]);
+            }
+        }
+        if (!a.lengths) {
+            buf0 += sdiv;
+            jb0 += smod;
+            if (jb0 >= bpb) {
+                jb0 -= bpb;
+                ++buf0;
+            }
+        }
+    }
+}
+
+#ifndef LCB_CHA_QUAD
+#define LCB_CHA_QUAD 0
+#endif
+
+// Workgroups that are resident at once on the whole device for kernel K
+// (CUs x occupancy), cached per device: the persistent grid is sized to it so
+// every wave runs from start to end and no partial second batch of waves
+// idles most SIMDs at the tail.
+template <class K>
+static uint64_t resident_grid(K kernel) {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cache[dev] <= 0) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0) per = 4;
+        cache[dev] = cus * per;
+    }
+    return (uint64_t)cache[dev];
+}
+
+template <int DR>
+static void launch_cha_dr(const ChaArgs& a, uint64_t need, hipStream_t s) {
+#if LCB_CHA_QUAD
+    auto kern = chacha_kernel<DR, LCB_CHA_B>;
+#else
+    auto kern = chacha_lane_kernel<DR>;
+#endif
+    uint64_t grid = std::min<uint64_t>(resident_grid(kern), need);
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 
 void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t* blk_start,
@@ -347,17 +628,16 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
                            subkeys);
         k.subkeys = subkeys;
     }
-    // Persistent grid: enough workgroups to fill 256 CUs several times over,
-    // fewer when the (known) fixed-layout total needs fewer tiles.
-    constexpr uint64_t kTile = 16u * LCB_CHA_B, kMaxGrid = 4096;
-    uint64_t grid = kMaxGrid;
-    if (!a.lengths) grid = std::min<uint64_t>(kMaxGrid, (a.total_blocks + 4 * kTile - 1) / (4 * kTile));
-    if (grid == 0) grid = 1;
+    // Persistent grid: the device's resident workgroup count, fewer when the
+    // (known) fixed-layout total needs fewer tiles.
+    constexpr uint64_t kTile = LCB_CHA_QUAD ? 16u * LCB_CHA_B : 64u;
+    uint64_t need = UINT64_MAX;
+    if (!a.lengths) need = (a.total_blocks + 4 * kTile - 1) / (4 * kTile);
     switch (a.dr) {
-    case 4: launch_cha_dr<4>(k, (unsigned)grid, s); break;     // ChaCha8
-    case 6: launch_cha_dr<6>(k, (unsigned)grid, s); break;     // ChaCha12
-    case 10: launch_cha_dr<10>(k, (unsigned)grid, s); break;   // ChaCha20
-    default: launch_cha_dr<0>(k, (unsigned)grid, s); break;
+    case 4: launch_cha_dr<4>(k, need, s); break;     // ChaCha8
+    case 6: launch_cha_dr<6>(k, need, s); break;     // ChaCha12
+    case 10: launch_cha_dr<10>(k, need, s); break;   // ChaCha20
+    default: launch_cha_dr<0>(k, need, s); break;
     }
 }
 

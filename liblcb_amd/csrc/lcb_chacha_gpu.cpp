@@ -64,6 +64,10 @@ int cha_enqueue(ChaArgs a, bool x, hipStream_t s) {
         if (a.fixed_len == 0) return 0;
         a.bpb = (uint32_t)((a.fixed_len + 63u) / 64u);
         a.total_blocks = (uint64_t)a.count * a.bpb;
+        // One dense run of whole, 16-B aligned blocks: the kernel's
+        // coalesced stream path applies to every full wave tile.
+        const uintptr_t al = reinterpret_cast<uintptr_t>(a.dst) | reinterpret_cast<uintptr_t>(a.src);
+        a.stream = (!a.offsets && a.stride == a.fixed_len && a.fixed_len % 64u == 0 && (al & 15u) == 0) ? 1u : 0u;
     }
     uint64_t* scan = nullptr;
     uint32_t* subkeys = nullptr;

@@ -54,6 +54,7 @@ struct ChaArgs {
     uint32_t fixed_len = 0, bpb = 1;
     uint32_t iv_words = 2, iv_at = 0;     // chacha 2,0; xchacha 6,4
     uint32_t dr = 10;                     // double rounds = ceil(rounds / 2)
+    uint32_t stream = 0;                  // dense aligned whole blocks: block g at byte 64 g
     uint32_t key[8] = {};                 // state words 4..11
     uint32_t cst[4] = {};                 // state words 0..3 of the block function
     uint32_t hcst[4] = {};                // state words 0..3 of hchacha (xchacha)

@@ -8,7 +8,7 @@ extra = sys.argv[1:]
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
                        "-S", "-o", "/tmp/cha.s", src] + extra)
 s = open("/tmp/cha.s").read()
-for m in re.finditer(r"^(_ZN6lcbgpu13chacha_kernel\w*):", s, re.M):
+for m in re.finditer(r"^(_ZN6lcbgpu\d+chacha_\w*kernel\w*):", s, re.M):
     end = s.index("s_endpgm", m.start())
     lines = [l.strip() for l in s[m.start():end].splitlines()[1:]]
     lines = [l for l in lines if l and not l.startswith((".", ";")) and not l.endswith(":")]
