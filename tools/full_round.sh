@@ -1,12 +1,16 @@
 #!/bin/bash
-# Round-end style GPU session: parity tests, bench, rocprofv3 trace of the
-# bench command, PMC passes (FETCH_SIZE, WRITE_SIZE) on the bench workload.
+# Round-end style GPU session: smoke, parity tests, bench, rocprofv3 trace of
+# the bench command, PMC passes (FETCH_SIZE, WRITE_SIZE, SQ group) on the
+# bench workload for every digest.  Stops at the first crash/timeout.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${TAG:-r1}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
-timeout -k 10 700 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err

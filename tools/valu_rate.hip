@@ -29,6 +29,11 @@
 #define OP_BFI(r) "v_bfi_b32 " r ", " r ", %8, %9\n"
 #define OP_OR3(r) "v_or3_b32 " r ", " r ", %8, %9\n"
 #define OP_CNDMASK(r) "v_cndmask_b32 " r ", " r ", %8, vcc\n"
+// Same VGPR read twice (a rotate is v_alignbit x, x, n).
+#define OP_ALIGNBIT_SAME(r) "v_alignbit_b32 " r ", " r ", " r ", 7\n"
+#define OP_PERM_SAME(r) "v_perm_b32 " r ", " r ", " r ", %9\n"
+#define OP_XOR_SAME(r) "v_xor_b32 " r ", " r ", " r "\n"
+#define OP_ADD_SAME(r) "v_add_u32 " r ", " r ", " r "\n"
 
 #define KERNEL(NAME, OP)                                                             \
     __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {          \
@@ -56,6 +61,10 @@ KERNEL(k_alignbyte, OP_ALIGNBYTE)
 KERNEL(k_mov, OP_MOV)
 KERNEL(k_bfi, OP_BFI)
 KERNEL(k_or3, OP_OR3)
+KERNEL(k_alignbit_same, OP_ALIGNBIT_SAME)
+KERNEL(k_perm_same, OP_PERM_SAME)
+KERNEL(k_xor_same, OP_XOR_SAME)
+KERNEL(k_add_same, OP_ADD_SAME)
 
 // 64-bit shifts and packed moves (rotate-by-64-bit-shift candidates).
 __global__ __launch_bounds__(256) void k_lshr64(unsigned* out, int iters) {
@@ -107,6 +116,59 @@ __global__ __launch_bounds__(256) void k_addc_pair(unsigned* out, int iters) {
     out[blockIdx.x * 256 + threadIdx.x] = l0 ^ h0 ^ l1 ^ h1;
 }
 
+// Two DISTINCT live VGPR sources per instruction (as in r_a += r_b of a
+// hash round), vs the single-live-source chains above.
+#define PAIR8(OP) OP("%0", "%4") OP("%1", "%5") OP("%2", "%6") OP("%3", "%7") \
+                  OP("%4", "%1") OP("%5", "%2") OP("%6", "%3") OP("%7", "%0")
+#define P_ADD(d, s) "v_add_u32 " d ", " d ", " s "\n"
+#define P_XOR(d, s) "v_xor_b32 " d ", " d ", " s "\n"
+#define P_BITOP3(d, s) "v_bitop3_b32 " d ", " d ", " s ", %8 bitop3:0x96\n"
+#define P_ADD3(d, s) "v_add3_u32 " d ", " d ", " s ", %8\n"
+#define P_ALIGNBIT(d, s) "v_alignbit_b32 " d ", " d ", " s ", 7\n"
+#define PAIRK(NAME, OP)                                                                   \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {               \
+        unsigned r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4,      \
+                 r5 = r0 + 5, r6 = r0 + 6, r7 = r0 + 7;                                   \
+        unsigned k0 = blockIdx.x | 1;                                                     \
+        for (int i = 0; i < iters; ++i) {                                                 \
+            asm volatile(REP8(PAIR8(OP))                                                  \
+                         : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5),     \
+                           "+v"(r6), "+v"(r7)                                              \
+                         : "v"(k0));                                                      \
+        }                                                                                 \
+        out[blockIdx.x * 256 + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;       \
+    }
+PAIRK(kp_add, P_ADD)
+PAIRK(kp_xor, P_XOR)
+PAIRK(kp_bitop3, P_BITOP3)
+PAIRK(kp_add3, P_ADD3)
+PAIRK(kp_alignbit, P_ALIGNBIT)
+
+// Mixes: full-rate add/xor with half-rate alignbit (the ChaCha / SHA mix).
+#define MIX_G(OP) OP("%0") OP("%1") OP("%2") OP("%3") OP("%4") OP("%5") OP("%6") OP("%7")
+#define M_ADD(r) "v_add_u32 " r ", " r ", %8\n"
+#define M_XOR(r) "v_xor_b32 " r ", " r ", %8\n"
+#define M_ROT(r) "v_alignbit_b32 " r ", " r ", " r ", 7\n"
+#define MIXK(NAME, BODY)                                                                   \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {               \
+        unsigned r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4,      \
+                 r5 = r0 + 5, r6 = r0 + 6, r7 = r0 + 7;                                   \
+        unsigned k0 = blockIdx.x | 1;                                                     \
+        for (int i = 0; i < iters; ++i) {                                                 \
+            asm volatile(BODY                                                             \
+                         : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5),     \
+                           "+v"(r6), "+v"(r7)                                              \
+                         : "v"(k0));                                                      \
+        }                                                                                 \
+        out[blockIdx.x * 256 + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;       \
+    }
+// 2 full : 1 half, grouped by 8 chains (24 instructions per group) x 8 = 192
+MIXK(km_grouped, REP8(MIX_G(M_ADD) MIX_G(M_XOR) MIX_G(M_ROT)))
+// 1 full : 1 half
+MIXK(km_1to1, REP8(MIX_G(M_XOR) MIX_G(M_ROT)))
+// all full
+MIXK(km_full, REP8(MIX_G(M_XOR) MIX_G(M_ADD)))
+
 typedef void (*kfn)(unsigned*, int);
 
 int main() {
@@ -120,7 +182,14 @@ int main() {
         {"v_add_co+addc (per instr)", k_addc_pair, 64},
         {"v_lshlrev_b32", k_shl, 64}, {"v_lshrrev_b32", k_shr, 64}, {"v_lshl_or_b32", k_lshlor, 64},
         {"v_alignbyte_b32", k_alignbyte, 64}, {"v_mov_b32", k_mov, 64}, {"v_bfi_b32", k_bfi, 64},
-        {"v_or3_b32", k_or3, 64}, {"v_lshrrev_b64", k_lshr64, 64}, {"v_pk_mov_b32", k_pkmov, 64}};
+        {"v_or3_b32", k_or3, 64}, {"v_lshrrev_b64", k_lshr64, 64}, {"v_pk_mov_b32", k_pkmov, 64},
+        {"v_alignbit_b32 x,x,x", k_alignbit_same, 64}, {"v_perm_b32 x,x,k", k_perm_same, 64},
+        {"v_xor_b32 x,x", k_xor_same, 64}, {"v_add_u32 x,x", k_add_same, 64},
+        {"2-live v_add_u32", kp_add, 64}, {"2-live v_xor_b32", kp_xor, 64},
+        {"2-live v_bitop3_b32", kp_bitop3, 64}, {"2-live v_add3_u32", kp_add3, 64},
+        {"2-live v_alignbit_b32", kp_alignbit, 64},
+        {"mix add+xor+alignbit (2:1)", km_grouped, 192}, {"mix xor+alignbit (1:1)", km_1to1, 128},
+        {"mix xor+add (full only)", km_full, 128}};
     int dev;
     hipGetDevice(&dev);
     int clk_khz;
