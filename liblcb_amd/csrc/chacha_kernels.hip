@@ -17,9 +17,8 @@
 // lane), and the keystream is redistributed lane-per-block -> lane-per-16-B
 // through a bank-conflict-free swizzled LDS slab.  Other layouts (ragged,
 // misaligned, partial blocks) go through per-lane 16-B / dword-slot /
-// byte paths.  The grid is persistent (grid-stride over 64-block wave
-// tiles), sized to the resident workgroup count, and every wave's exit
-// condition is the block total it reads.
+// byte paths.  Waves grid-stride over 64-block tiles, a few tiles each, and
+// every wave's exit condition is the block total it reads.
 //
 // chacha_kernel (compiled out, LCB_CHA_QUAD=1): FOUR LANES PER BLOCK, lane q
 // holding column q; the diagonal round rotates rows 1-3 by DPP quad_perm
@@ -425,9 +424,15 @@ __global__ __launch_bounds__(256) void chacha_lane_kernel(ChaArgs a) {
     const uint64_t gstep = nwaves * kTile;
     uint64_t buf0 = 0, jb0 = 0, sdiv = 0, smod = 0;
     if (!a.lengths) {
-        buf0 = (wave0 * kTile) / bpb;
+        if (total <= 0xffffffffull && gstep <= 0xffffffffull) {  // wave-uniform: 32-bit divisions
+            const uint32_t q0 = (uint32_t)(wave0 * kTile) / (uint32_t)bpb, q1 = (uint32_t)gstep / (uint32_t)bpb;
+            buf0 = q0;
+            sdiv = q1;
+        } else {
+            buf0 = (wave0 * kTile) / bpb;
+            sdiv = gstep / bpb;
+        }
         jb0 = wave0 * kTile - buf0 * bpb;
-        sdiv = gstep / bpb;
         smod = gstep - sdiv * bpb;
     }
     for (uint64_t t = wave0; t * kTile < total; t += nwaves) {
@@ -600,15 +605,26 @@ static uint64_t resident_grid(K kernel) {
     return (uint64_t)cache[dev];
 }
 
+// Grid: each wave takes ~kTilesPerWave tiles (grid-stride), so a launch is
+// many short waves rather than exactly one resident batch — the hardware
+// dispatcher then evens out the tail, and nothing depends on the occupancy
+// API (which can over-count residency by one workgroup per CU at some SGPR
+// counts, MI355X_MICROARCH.md 'Residency').  Ragged batches (total unknown on
+// the host) launch 8x the resident count and grid-stride.
+#ifndef LCB_CHA_TILES_PER_WAVE
+#define LCB_CHA_TILES_PER_WAVE 4
+#endif
 template <int DR>
-static void launch_cha_dr(const ChaArgs& a, uint64_t need, hipStream_t s) {
+static void launch_cha_dr(const ChaArgs& a, uint64_t need_tiles, hipStream_t s) {
 #if LCB_CHA_QUAD
     auto kern = chacha_kernel<DR, LCB_CHA_B>;
 #else
     auto kern = chacha_lane_kernel<DR>;
 #endif
-    uint64_t grid = std::min<uint64_t>(resident_grid(kern), need);
-    if (grid == 0) grid = 1;
+    uint64_t grid = need_tiles == UINT64_MAX
+                        ? 8 * resident_grid(kern)
+                        : (need_tiles + 4 * LCB_CHA_TILES_PER_WAVE - 1) / (4 * LCB_CHA_TILES_PER_WAVE);
+    grid = std::min<uint64_t>(std::max<uint64_t>(grid, 1), 1u << 20);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
 
@@ -628,11 +644,10 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
                            subkeys);
         k.subkeys = subkeys;
     }
-    // Persistent grid: the device's resident workgroup count, fewer when the
-    // (known) fixed-layout total needs fewer tiles.
+    // Grid sizing: see launch_cha_dr.
     constexpr uint64_t kTile = LCB_CHA_QUAD ? 16u * LCB_CHA_B : 64u;
-    uint64_t need = UINT64_MAX;
-    if (!a.lengths) need = (a.total_blocks + 4 * kTile - 1) / (4 * kTile);
+    uint64_t need = UINT64_MAX;  // tiles
+    if (!a.lengths) need = (a.total_blocks + kTile - 1) / kTile;
     switch (a.dr) {
     case 4: launch_cha_dr<4>(k, need, s); break;     // ChaCha8
     case 6: launch_cha_dr<6>(k, need, s); break;     // ChaCha12

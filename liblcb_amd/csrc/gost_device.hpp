@@ -4,9 +4,10 @@
 // One lane per message (as the MD family).  The LPS transform uses the
 // big-table form of the reference (gost3411-2012.h:1071-1099):
 //     dst[i] = XOR_{j=0..7} Ax[j][ byte i of src[j] ]
-// with the 8 x 256 x u64 = 16 KiB table held in LDS (one copy per workgroup),
-// so LPS is 64 ds_read_b64 + 56 XORs per 512-bit transform and a 64-byte
-// block costs 25 LPS (gost3411-2012.h:1129-1142).  The table is generated at
+// with the 8 x 256 x u64 = 16 KiB table held in LDS — in the batch kernels
+// as a 64 KiB lane-rotated, bank-sliced image (GostRot below) whose gathers
+// are bank-conflict-free — so LPS is 64 ds_read_b64 + XORs per 512-bit
+// transform and a 64-byte block costs 25 LPS (gost3411-2012.h:1129-1142).  The table is generated at
 // COMPILE TIME from the RFC 6986 S-box pi and the 64 rows of the linear map A,
 // following the reference's small-table definition (gost3411-2012.h:1032-1067),
 // and pinned against the reference's gost3411_2012_Ax by a test.
@@ -144,32 +145,112 @@ __device__ __forceinline__ void gost_lps(uint64_t o[8], const uint64_t x[8], con
     }
 }
 
+// The flat table (one 16 KiB copy, entry (j, b) at T[j * 256 + b]): the
+// one-lane HMAC key-schedule prep kernel.
+struct GostFlat {
+    const uint64_t* T;
+    __device__ __forceinline__ void lps(uint64_t o[8], const uint64_t x[8]) const { gost_lps(o, x, T); }
+};
+
+// Lane-rotated, bank-sliced LPS table (the batch kernels).
+//
+// With the flat table the 64 data-dependent ds_read_b64 of an LPS land on
+// random bank pairs: a 32-lane group meets ~3.4 distinct entries on its
+// busiest bank pair, ~6.5 LDS cycles per wave-instruction instead of 2
+// (DESIGN.md 5).  Here the LDS holds 4 replicas of the 8 tables, table j of
+// replica c alone in bank pair 8c + j (entry b at byte b * 256 + (8c + j) * 8,
+// 64 KiB), and lane l (c = (l & 31) >> 3, r = l & 7) takes the 8 input words
+// of an LPS in the rotated order j = (j' + r) & 7 at static step j'.  At every
+// step the 32 lanes of a ds_read_b64 group then read 32 different bank
+// pairs: conflict-free whatever the data.  The rotation is a 3-stage barrel
+// over the lane's 8 input words (bit-selects); a lookup address is ONE
+// v_perm_b32 (table byte -> address bits 8-15, the lane's bank-pair offset
+// -> bits 0-7), one instruction fewer than the flat form's extract + shift.
+using lds_u8 = __attribute__((address_space(3))) const uint8_t;
+using lds_u64 = __attribute__((address_space(3))) const uint64_t;
+
+struct GostRot {
+    lds_u8* L;
+    uint32_t off[8];     // (8c + ((j' + r) & 7)) * 8
+    uint32_t m1, m2, m4;  // all-ones where bit 0 / 1 / 2 of r is set
+    __device__ __forceinline__ void init(lds_u8* lds) {
+        L = lds;
+        const uint32_t l = threadIdx.x & 31u, c = l >> 3, r = l & 7u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) off[j] = (8u * c + (((uint32_t)j + r) & 7u)) * 8u;
+        m1 = (r & 1u) ? 0xffffffffu : 0u;
+        m2 = (r & 2u) ? 0xffffffffu : 0u;
+        m4 = (r & 4u) ? 0xffffffffu : 0u;
+    }
+    template <int S>
+    __device__ __forceinline__ static void rot(uint32_t (&v)[8], uint32_t m) {  // v[j] <- v[(j + S) & 7] where m
+        uint32_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = ch3(m, v[(j + S) & 7], v[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = t[j];
+    }
+    // LPS(x) (gost3411-2012.h:1071-1090): o[i] = XOR_j Ax[j][byte i of x[j]].
+    __device__ __forceinline__ void lps(uint64_t o[8], const uint64_t x[8]) const {
+        uint32_t lo[8], hi[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { lo[j] = (uint32_t)x[j]; hi[j] = (uint32_t)(x[j] >> 32); }
+        rot<1>(lo, m1); rot<1>(hi, m1);
+        rot<2>(lo, m2); rot<2>(hi, m2);
+        rot<4>(lo, m4); rot<4>(hi, m4);   // lo/hi[j'] = word (j' + r) & 7
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            // address bytes: [0] = off (S1 byte 0), [1] = byte i&3 of the word (S0), [2,3] = 0
+            const uint32_t sel = 0x0c0c0000u | ((4u + (uint32_t)(i & 3)) << 8);
+            uint64_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t a = __builtin_amdgcn_perm((i < 4) ? lo[j] : hi[j], off[j], sel);
+                v[j] = *reinterpret_cast<lds_u64*>(L + a);
+            }
+            uint32_t l = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]),
+                              xor3((uint32_t)v[3], (uint32_t)v[4], (uint32_t)v[5]),
+                              (uint32_t)v[6] ^ (uint32_t)v[7]);
+            uint32_t h = xor3(xor3((uint32_t)(v[0] >> 32), (uint32_t)(v[1] >> 32), (uint32_t)(v[2] >> 32)),
+                              xor3((uint32_t)(v[3] >> 32), (uint32_t)(v[4] >> 32), (uint32_t)(v[5] >> 32)),
+                              (uint32_t)(v[6] >> 32) ^ (uint32_t)(v[7] >> 32));
+            o[i] = ((uint64_t)h << 32) | l;
+        }
+    }
+};
+
+// Fills the 64 KiB rotated image (every thread, then barrier).
+__device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGostAxDev.t[i & 7][i >> 5];
+    __syncthreads();
+}
+
 // g_N(h, m) for a counter N whose upper 448 bits are zero (messages shorter
 // than 2^61 bytes; the ABI caps lengths at 2^32): gost3411-2012.h:1110-1144.
-__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8],
-                                       const uint64_t* __restrict__ T) {
+template <class Tab>
+__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
     uint64_t k[8], t[8], x[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = h[i];
     x[0] ^= n0;
-    gost_lps(k, x, T);                                   // K = LPS(h ^ N)
+    T.lps(k, x);                                         // K = LPS(h ^ N)
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = k[i] ^ m[i];
-    gost_lps(t, x, T);                                   // t = LPS(K ^ m)
+    T.lps(t, x);                                         // t = LPS(K ^ m)
     // Rounds 1..11: K = LPS(K ^ C_{r-1}); t = LPS(t ^ K).  Kept rolled: the
     // body is 128 LDS lookups already, the constants are wave-uniform loads.
 #pragma unroll 1
     for (int r = 0; r < 11; ++r) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[r][i];
-        gost_lps(k, x, T);                               // K = LPS(K ^ C_r)
+        T.lps(k, x);                                     // K = LPS(K ^ C_r)
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = t[i] ^ k[i];
-        gost_lps(t, x, T);                               // t = LPS(t ^ K)
+        T.lps(t, x);                                     // t = LPS(t ^ K)
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[11][i];
-    gost_lps(k, x, T);                                   // K13 = LPS(K ^ C_11)
+    T.lps(k, x);                                         // K13 = LPS(K ^ C_11)
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] ^= m[i] ^ t[i] ^ k[i];  // :1142
 }
@@ -184,7 +265,8 @@ struct Gost {
         n0 = 0;
     }
     // One g_N step over raw LE words w (gost3411-2012.h:1129-1131).
-    __device__ __forceinline__ void block(const uint32_t* w, uint64_t bits, const uint64_t* T) {
+    template <class Tab>
+    __device__ __forceinline__ void block(const uint32_t* w, uint64_t bits, const Tab& T) {
         uint64_t m[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
@@ -202,7 +284,8 @@ struct Gost {
         }
     }
     // Tail + finalisation (gost3411-2012.h:1820-1839).
-    __device__ __forceinline__ void finish(uint32_t* w, uint32_t rem, const uint64_t* T) {
+    template <class Tab>
+    __device__ __forceinline__ void finish(uint32_t* w, uint32_t rem, const Tab& T) {
         put_byte(w, rem, 0x01u);
         block(w, (uint64_t)rem * 8u, T);
         uint64_t m[8];
@@ -239,9 +322,8 @@ struct Gost {
 };
 
 // Whole message through a GOST state (gost3411_2012_update + _final).
-template <bool k256>
-__device__ __forceinline__ void gost_message(Gost<k256>& st, const uint8_t* msg, uint64_t len,
-                                             const uint64_t* T) {
+template <bool k256, class Tab>
+__device__ __forceinline__ void gost_message(Gost<k256>& st, const uint8_t* msg, uint64_t len, const Tab& T) {
     uint32_t w[16];
     const uint64_t nfull = len / 64;
     const uint8_t* p = msg;

@@ -47,6 +47,25 @@
 #ifndef LCB_PAIR_SHA256
 #define LCB_PAIR_SHA256 0
 #endif
+// GOST batch kernels: lane-rotated bank-sliced LPS image (gost_device.hpp)
+// instead of the flat 16 KiB table.
+#ifndef LCB_GOST_ROT
+#define LCB_GOST_ROT 1
+#endif
+// Non-temporal (nt) policy on the once-read message stream (A/B knob).
+#ifndef LCB_NT
+#define LCB_NT 0
+#endif
+__device__ __forceinline__ uint4 stream_load16(const uint4* p) {
+#if LCB_NT
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+#define LCB_STREAM_LOAD(p) stream_load16(p)
 #ifndef LCB_OCC_GOST
 #define LCB_OCC_GOST 2
 #endif
@@ -160,7 +179,7 @@ __device__ __forceinline__ void load_full128(const uint8_t* p, uint32_t w0[16], 
         const uint4* q = reinterpret_cast<const uint4*>(p);
         uint4 v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = q[k];
+        for (int k = 0; k < 8; ++k) v[k] = LCB_STREAM_LOAD(&q[k]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             w0[4 * k + 0] = v[k].x; w0[4 * k + 1] = v[k].y; w0[4 * k + 2] = v[k].z; w0[4 * k + 3] = v[k].w;

@@ -79,6 +79,7 @@ size_t dsize(int alg);                  // digest bytes, 0 for an unknown alg
 size_t bsize(int alg);                  // block bytes (HMAC key block)
 int map_err(hipError_t e);              // HIP error -> liblcb errno code
 int ensure_init();                      // 0, or ENODEV without a usable device
+int device_cu_count();                  // compute units of the current device (cached)
 // Enqueue the HMAC mid-state prep; *mid / *dkey are stream-ordered
 // allocations the caller releases with hipFreeAsync after its last use.
 int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,

@@ -159,8 +159,16 @@ __global__ void md_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t k
 // ------------------------------------------------------------------ GOST
 template <bool k256, bool kHmac>
 __global__ __launch_bounds__(256, LCB_OCC_GOST) void gost_batch_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint64_t T[8 * 256];
-    gost_stage_table(T);
+#if LCB_GOST_ROT
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
+    gost_stage_rot(Timg);
+    GostRot T;
+    T.init((lds_u8*)Timg);
+#else
+    __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
+    gost_stage_table(Timg);
+    const GostFlat T{Timg};
+#endif
     uint64_t idx, len;
     const uint8_t* msg;
     if (!msg_at(a, idx, msg, len)) return;
@@ -196,8 +204,9 @@ __global__ __launch_bounds__(256, LCB_OCC_GOST) void gost_batch_kernel(KArgs a) 
 
 template <bool k256>
 __global__ void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid) {
-    __shared__ __attribute__((aligned(16))) uint64_t T[8 * 256];
-    gost_stage_table(T);
+    __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
+    gost_stage_table(Timg);
+    const GostFlat T{Timg};
     if (threadIdx.x != 0) return;
     using G = Gost<k256>;
     uint32_t k[16];
