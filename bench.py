@@ -48,7 +48,7 @@ MSGS_PER_GPU = 1 << 20
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--alg", default="md5", choices=sorted(ALG_IDS))
     p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU")
@@ -256,7 +256,7 @@ def bench_crc(data, count, steps):
 def bench_chacha(data, count, steps):
     """ChaCha / XChaCha (include/crypto/cipher/chacha.h)
     over the same 1M x 1 KiB device-resident bytes, iv_i = i: per-variant
-    kernel time (HIP events on the launch stream, after 3 warm launches) and
+    kernel time (HIP events on the launch stream, after 30 warm launches) and
     HBM fraction of the algorithmic bytes (count x (1024 read + 1024 written
     + 8 B iv); keystream-only: 1024 written + 8)."""
     dst = torch.empty_like(data)
@@ -274,7 +274,7 @@ def bench_chacha(data, count, steps):
             check(lib().lcb_chacha_batch(x, key, 32, None, iv.data_ptr(), rounds,
                                          data.data_ptr() if enc else None, dst.data_ptr(), None, None,
                                          count, MSG_LEN, MSG_LEN, F_DEVICE, stream.cuda_stream))
-        for _ in range(10):
+        for _ in range(30):
             launch()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
@@ -380,6 +380,7 @@ def main():
         out["per_alg"] = per
         out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
         out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
+        settle()   # ChaCha20 is VALU-heavy: let the clock settle after the HBM-bound CRC launches
         out["chacha"] = bench_chacha(data, count, max(3, a.steps // 4))
         out["ingest"] = bench_ingest(alg)
         # End-to-end host path on the same bytes (lcb_hash_batch host mode):

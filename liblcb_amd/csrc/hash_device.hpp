@@ -34,13 +34,17 @@
 #ifndef LCB_OCC_SHA512
 #define LCB_OCC_SHA512 4
 #endif
-// LDS-DMA staged fixed-stride kernel (lcb_kernels.hip): parity-green but
-// measured performance-neutral vs direct 128-B line loads on MI355X (MD5
-// 0.21 vs 0.20-0.21 ms per 1 GiB, both ~90% of the 5.9 TB/s streaming read
-// rate of tools/loadpat.hip) while capping occupancy at 5 waves/SIMD; off.
+// LDS-DMA staged fixed-stride kernel (lcb_kernels.hip) for MD5/SHA-1: with
+// the default cache policy it measured equal to direct 128-B line loads; with
+// the nt policy on the DMA stream (LCB_LDS_AUX = 2, lcb_kernels.hip) it is
+// 1.6 % faster on MD5 and SHA-1 (two A/B sessions, back-to-back launches,
+// profiles/r1_md5_variants_ab.txt), so it is the fixed-stride path.
 #ifndef LCB_FIXED_LDS
-#define LCB_FIXED_LDS 0
+#define LCB_FIXED_LDS 1
 #endif
+// Register ping-pong prefetch of the next 128-B line in md_message: at the
+// 8-wave VGPR cap it spills (303 VGPRs to scratch, 3.5x slower); at a 4-wave
+// cap it fits (116 VGPRs) and is 3 % slower than no prefetch.  Off.
 #ifndef LCB_PREFETCH
 #define LCB_PREFETCH 0
 #endif

@@ -9,6 +9,10 @@
 #include "gost_device.hpp"
 #include "lcb_internal.hpp"
 
+#ifndef LCB_LDS_AUX
+#define LCB_LDS_AUX 2   // cache-policy bits of the LDS-DMA stream: nt (each byte is read once)
+#endif
+
 namespace lcbgpu {
 
 __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds(
                 (__attribute__((address_space(1))) void*)(src[g] + L * 128),
-                (__attribute__((address_space(3))) void*)(my + g * 1024), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(my + g * 1024), 16, 0, LCB_LDS_AUX);
     };
     H st;
     uint64_t prefix = 0;

@@ -16,7 +16,7 @@ from liblcb_amd._lib import ALG_IDS, DIGEST_SIZE, F_DEVICE, check, lib  # noqa: 
 
 p = argparse.ArgumentParser()
 p.add_argument("--alg", default="md5")
-p.add_argument("--reps", type=int, default=10)
+p.add_argument("--reps", type=int, default=50)
 p.add_argument("--count", type=int, default=1 << 20)
 p.add_argument("--len", type=int, default=1024)
 p.add_argument("--warmup", type=int, default=60, help="untimed launches per algorithm (clock ramp)")
@@ -31,15 +31,14 @@ for name in a.alg.split(","):
     for _ in range(a.warmup):
         check(lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), None, None, a.count, a.len, a.len,
                                    dig.data_ptr(), F_DEVICE, s.cuda_stream))
-    for r in range(a.reps + 1):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+    for e0, e1 in ev:      # back to back, as bench.py times them
         e0.record(s)
         check(lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), None, None, a.count, a.len, a.len,
                                    dig.data_ptr(), F_DEVICE, s.cuda_stream))
         e1.record(s)
-        torch.cuda.synchronize()
-        if r:
-            ts.append(e0.elapsed_time(e1))
+    torch.cuda.synchronize()
+    ts = [e0.elapsed_time(e1) for e0, e1 in ev]
     ts.sort()
     gb = a.count * a.len
     print("%-8s median %.4f ms  min %.4f ms  %.1f GB/s (min)" % (name, ts[len(ts) // 2], ts[0],
