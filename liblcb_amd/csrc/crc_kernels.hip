@@ -59,6 +59,43 @@ __global__ __launch_bounds__(1024) void crc_priv_kernel(KArgs a) {
     }
 }
 
+// Fixed-stride batches (lcb_internal.hpp fixed_stride_lines): the 128-B lines
+// arrive through the per-wave LDS-DMA line stream (LdsLineStream,
+// hash_device.hpp), line L+1 in flight while line L is folded in.
+template <int V>
+__global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
+    using Var = CrcVar<V>;
+    __shared__ uint32_t T[8 * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    crc_stage_tables(T, Var::kFam);  // before any early return: it synchronises
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    if (wave_first >= a.count) return;  // wave-uniform
+    const uint64_t last = a.count - 1, nlines = a.fixed_len / 128;
+    LdsLineStream ls;
+    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
+    const uint64_t i = wave_first + lane, ic = i > last ? last : i;
+    const uint32_t c = a.init ? gptr(a.init)[ic] : Var::kOneshot;
+    const CrcRule<Var::kRefl> R{T};
+    uint32_t r = Var::kInv ? ~c : c;
+    if (nlines) ls.issue(0);
+    for (uint64_t L = 0; L < nlines; ++L) {
+        uint32_t w0[16], w1[16];
+        ls.take(w0, w1);
+        if (L + 1 < nlines) ls.issue(L + 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r = R.step8(r, w0[2 * j], w0[2 * j + 1]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r = R.step8(r, w1[2 * j], w1[2 * j + 1]);
+    }
+    if (i > last) return;
+    r = crc_message(R, r, gptr(a.data) + i * a.stride + nlines * 128, (uint64_t)a.fixed_len - nlines * 128);
+    gptr(reinterpret_cast<uint32_t*>(a.digests))[i] = Var::kInv ? ~r : r;
+}
+
+#ifndef LCB_CRC_FIXED_LDS
+#define LCB_CRC_FIXED_LDS 1
+#endif
 #ifndef LCB_CRC_PRIV
 #define LCB_CRC_PRIV 0
 #endif
@@ -71,7 +108,10 @@ static void launch_crc_v(const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(crc_priv_kernel<V>, dim3((unsigned)grid), dim3(1024), 0, s, a);
 #else
     const uint64_t blocks = (a.count + 255) / 256;
-    hipLaunchKernelGGL(crc_batch_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    if (LCB_CRC_FIXED_LDS && fixed_stride_lines(a))
+        hipLaunchKernelGGL(crc_fixed_lds_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(crc_batch_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
 #endif
 }
 

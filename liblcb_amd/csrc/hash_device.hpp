@@ -583,6 +583,60 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // Processes a whole message of `len` bytes starting from state `st`, whose
 // compressed prefix is `prefix` bytes long (0, or the block for HMAC inner),
 // then pads (md5.h:266-288 / sha1.h:816-840 / sha2.h:706-742).
+// Per-wave LDS-DMA line stream over 64 fixed-stride records (the fixed-stride
+// fast paths of lcb_kernels.hip and crc_kernels.hip).  The per-lane loads of
+// the generic kernels touch 64 different 128-B lines per wave-instruction;
+// here line L of the wave's 64 records moves into an 8 KiB LDS slab with 8
+// coalesced LDS-DMA instructions (global_load_lds_dwordx4: one instruction =
+// 8 records x one whole 128-B line), every lane copies its own 128 B into
+// VGPRs (take), and the caller issues line L+1 before computing line L.
+// 16-B chunks are XOR-swizzled (chunk k of local record j sits in slot
+// k ^ ((j >> 1) & 7)) so the 16-lane ds_read_b128 groups are conflict-free.
+// Lanes beyond the last record load the last record (clamped) and must not
+// store.  The DMA stream carries the nt cache policy (every byte is read
+// once; LCB_LDS_AUX).
+#ifndef LCB_LDS_AUX
+#define LCB_LDS_AUX 2
+#endif
+struct LdsLineStream {
+    const uint8_t* src[8];
+    uint8_t* slab;
+    uint32_t lane;
+    __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first,
+                                         uint64_t last, uint32_t ln, uint8_t* my_slab) {
+        lane = ln;
+        slab = my_slab;
+        // DMA sources: instruction g carries local records 8g .. 8g+7; this lane
+        // moves chunk ((lane & 7) ^ f) of record 8g + (lane >> 3), f = (4g + (lane >> 4)) & 7.
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            uint64_t j = wave_first + 8 * g + (lane >> 3);
+            j = j > last ? last : j;
+            const uint32_t f = ((lane >> 4) + 4 * g) & 7;
+            src[g] = data + j * stride + ((lane & 7) ^ f) * 16;
+        }
+    }
+    __device__ __forceinline__ void issue(uint64_t L) const {
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + L * 128),
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             LCB_LDS_AUX);
+    }
+    // Waits for the issued line, copies this lane's 128 B (raw LE words).
+    __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16]) const {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line landed
+        const uint32_t fj = (lane >> 1) & 7;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 v = *reinterpret_cast<const uint4*>(slab + lane * 128 + ((k ^ fj) * 16));
+            uint32_t* d = (k < 4) ? (w0 + 4 * k) : (w1 + 4 * (k - 4));
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab free again
+    }
+};
+
 template <class H>
 __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
     uint32_t w[H::kWords];

@@ -21,6 +21,13 @@ struct KArgs {
     const uint32_t* init = nullptr;  // CRC: per-buffer X_update() value (nullptr: one-shot X())
 };
 
+// Fixed-stride batch of 16-B aligned records with at least one whole 128-B
+// line each: the shape the LDS-DMA line-stream kernels accept.
+inline bool fixed_stride_lines(const KArgs& a) {
+    return !a.offsets && !a.lengths && !a.order && (a.stride % 16) == 0 &&
+           (reinterpret_cast<uintptr_t>(a.data) % 16) == 0 && a.fixed_len >= 128 && a.stride >= a.fixed_len;
+}
+
 // Words reserved per HMAC mid-state (GOST needs 34: h, N, Sigma).
 constexpr int kMidWords = 64;
 

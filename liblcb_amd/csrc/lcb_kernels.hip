@@ -9,10 +9,6 @@
 #include "gost_device.hpp"
 #include "lcb_internal.hpp"
 
-#ifndef LCB_LDS_AUX
-#define LCB_LDS_AUX 2   // cache-policy bits of the LDS-DMA stream: nt (each byte is read once)
-#endif
-
 namespace lcbgpu {
 
 __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
@@ -50,19 +46,10 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 
 // ------------------------------------------- MD family, fixed-stride fast path
 // Fixed-stride batches with 16-B aligned records of >= 128 bytes (the bench
-// workload and any array of equal-size records).  The per-lane loads of the
-// generic kernel touch 64 different 128-B lines per wave-instruction, which
-// caps the HBM read rate (tools/loadpat.hip: 4.4 TB/s for that pattern vs
-// 5.6-5.9 TB/s coalesced).  Here each wave streams its 64 records' line L
-// into an 8 KiB LDS slab with 8 coalesced LDS-DMA instructions
-// (global_load_lds_dwordx4: one instruction = 8 records x one whole 128-B
-// line), every lane copies its own 128 B into VGPRs, the DMA of line L+1 is
-// issued, and the two 64-B blocks of line L are compressed while it lands.
-// 16-B chunks are XOR-swizzled (chunk k of local record j sits in slot
-// k ^ ((j >> 1) & 7)) so the 16-lane ds_read_b128 groups are conflict-free.
-// Lanes beyond `count` still issue DMAs (clamped to the last record) and
-// never store.  Bytes after the last whole line go through the generic
-// loader.
+// workload and any array of equal-size records): each wave streams line L+1
+// of its 64 records into LDS (LdsLineStream, hash_device.hpp) while the two
+// 64-B blocks of line L are compressed.  Bytes after the last whole line go
+// through the generic loader.
 template <class H, bool kHmac>
 __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
@@ -71,24 +58,8 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     if (wave_first >= a.count) return;  // wave-uniform
     const uint64_t last = a.count - 1;
     const uint64_t nlines = a.fixed_len / 128;
-    uint8_t* my = &slab[wv][0];
-    // DMA sources: instruction g carries local records 8g .. 8g+7; this lane
-    // moves chunk ((lane & 7) ^ f) of record 8g + (lane >> 3), f = (4g + (lane >> 4)) & 7.
-    const uint8_t* src[8];
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        uint64_t j = wave_first + 8 * g + (lane >> 3);
-        j = j > last ? last : j;
-        const uint32_t f = ((lane >> 4) + 4 * g) & 7;
-        src[g] = a.data + j * a.stride + ((lane & 7) ^ f) * 16;
-    }
-    auto issue = [&](uint64_t L) {
-#pragma unroll
-        for (int g = 0; g < 8; ++g)
-            __builtin_amdgcn_global_load_lds(
-                (__attribute__((address_space(1))) void*)(src[g] + L * 128),
-                (__attribute__((address_space(3))) void*)(my + g * 1024), 16, 0, LCB_LDS_AUX);
-    };
+    LdsLineStream ls;
+    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
     H st;
     uint64_t prefix = 0;
     if (kHmac) {
@@ -97,19 +68,11 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     } else {
         st.init();
     }
-    if (nlines) issue(0);
-    const uint32_t fj = (lane >> 1) & 7;
+    if (nlines) ls.issue(0);
     for (uint64_t L = 0; L < nlines; ++L) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line L landed
         uint32_t w0[16], w1[16];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(my + lane * 128 + ((k ^ fj) * 16));
-            uint32_t* d = (k < 4) ? (w0 + 4 * k) : (w1 + 4 * (k - 4));
-            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab free again
-        if (L + 1 < nlines) issue(L + 1);
+        ls.take(w0, w1);                 // line L -> VGPRs, slab free again
+        if (L + 1 < nlines) ls.issue(L + 1);
         st.compress(w0);
         st.compress(w1);
     }
@@ -345,11 +308,7 @@ static inline dim3 grid_for(uint64_t count) { return dim3((unsigned)((count + 25
 
 // The LDS-DMA fast path applies to fixed-stride, 16-B aligned records of at
 // least one whole 128-B line, for the HBM-bound 64-B-block algorithms.
-static bool fixed_lds_ok(const KArgs& a) {
-    return LCB_FIXED_LDS && !a.offsets && !a.lengths && !a.order &&
-           (a.stride % 16) == 0 && (reinterpret_cast<uintptr_t>(a.data) % 16) == 0 &&
-           a.fixed_len >= 128 && a.stride >= a.fixed_len;
-}
+static bool fixed_lds_ok(const KArgs& a) { return LCB_FIXED_LDS && fixed_stride_lines(a); }
 
 template <class H>
 static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {

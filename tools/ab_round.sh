@@ -8,7 +8,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/ab/tests.log
 for v in main ${VARIANTS:-old nt}; do
   if [ $v = main ]; then L=""; else L=$PWD/build_exp/lib_$v.so; fi
   echo "== $v"
-  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/kbench.py --alg ${ALGS:-md5,gost256,gost512} --reps 10 || exit 1
-  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/crc_bench.py --variants 1,4,6 --reps 10 || exit 1
-  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/cha_bench.py --rounds 20,8 --reps 10 || exit 1
+  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/kbench.py --alg ${ALGS:-md5,gost256,gost512} --reps 30 || exit 1
+  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/crc_bench.py --variants 1,4,6 --reps 30 || exit 1
+  LCB_HASH_GPU_LIB=$L timeout -k 10 120 python3 tools/cha_bench.py --rounds 20,8 --reps 30 || exit 1
 done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/ab/bench.log
