@@ -51,6 +51,15 @@
 #ifndef LCB_PAIR_SHA256
 #define LCB_PAIR_SHA256 0
 #endif
+// LDS-DMA line stream for fixed-stride SHA-224/256 and SHA-384/512 batches:
+// A/B (profiles/r1_sha2_lds_ab.txt) SHA-224/256 2.4 % faster (on), SHA-384/512
+// 2.5-4 % slower (3 waves/SIMD at 139 VGPRs instead of 4; off).
+#ifndef LCB_LDS_SHA256
+#define LCB_LDS_SHA256 1
+#endif
+#ifndef LCB_LDS_SHA512
+#define LCB_LDS_SHA512 0
+#endif
 // GOST batch kernels: lane-rotated bank-sliced LPS image (gost_device.hpp)
 // instead of the flat 16 KiB table.
 #ifndef LCB_GOST_ROT
@@ -227,6 +236,7 @@ __device__ __forceinline__ void put_byte(uint32_t w[16], uint32_t pos, uint32_t 
 struct Md5 {
     static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_MD5;
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
+    static constexpr bool kLdsStream = true;  // fixed-stride batches: LDS-DMA line stream
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -330,6 +340,7 @@ struct Md5 {
 struct Sha1 {
     static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_SHA1;
     static constexpr bool kPairLoad = true;
+    static constexpr bool kLdsStream = true;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -388,6 +399,7 @@ struct Sha256 {
     static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16,
                          kOcc = LCB_OCC_SHA256;
     static constexpr bool kPairLoad = LCB_PAIR_SHA256;  // VALU-bound: fewer live VGPRs
+    static constexpr bool kLdsStream = LCB_LDS_SHA256;
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -465,6 +477,7 @@ struct Sha512 {
     static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32,
                          kOcc = LCB_OCC_SHA512;
     static constexpr bool kPairLoad = false;  // 128-B blocks already
+    static constexpr bool kLdsStream = LCB_LDS_SHA512;
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143

@@ -70,11 +70,15 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     }
     if (nlines) ls.issue(0);
     for (uint64_t L = 0; L < nlines; ++L) {
-        uint32_t w0[16], w1[16];
-        ls.take(w0, w1);                 // line L -> VGPRs, slab free again
+        uint32_t w[32];
+        ls.take(w, w + 16);              // line L -> VGPRs, slab free again
         if (L + 1 < nlines) ls.issue(L + 1);
-        st.compress(w0);
-        st.compress(w1);
+        if constexpr (H::kBlock == 128) {
+            st.compress(w);              // one SHA-384/512 block per line
+        } else {
+            st.compress(w);              // two 64-B blocks per line
+            st.compress(w + 16);
+        }
     }
     const uint64_t i = wave_first + lane;
     if (i > last) return;
@@ -312,7 +316,7 @@ static bool fixed_lds_ok(const KArgs& a) { return LCB_FIXED_LDS && fixed_stride_
 
 template <class H>
 static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
-    if constexpr (H::kPairLoad) {
+    if constexpr (H::kLdsStream) {
         if (fixed_lds_ok(a)) {
             if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
             else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
