@@ -48,6 +48,11 @@
 #ifndef LCB_PREFETCH
 #define LCB_PREFETCH 0
 #endif
+// Fixed-length batches whose length is a whole number of blocks end in a
+// pad-only block built from the (wave-uniform) length: md_pad_only.
+#ifndef LCB_UNIFORM_PAD
+#define LCB_UNIFORM_PAD 1
+#endif
 #ifndef LCB_PAIR_SHA256
 #define LCB_PAIR_SHA256 0
 #endif
@@ -120,6 +125,15 @@ __device__ __forceinline__ uint32_t ch3(uint32_t x, uint32_t y, uint32_t z) {   
 __device__ __forceinline__ uint32_t maj3(uint32_t x, uint32_t y, uint32_t z) {  // majority
     return __builtin_amdgcn_bitop3_b32(x, y, z, 0xe8);
 }
+// Plain-C forms for wave-uniform operands: no VALU-only builtins, so values
+// derived from kernel arguments stay on the scalar ALU (s_lshr/s_lshl/s_or).
+// (A 32-bit rotate written as shifts is re-formed into rotr, which only has a
+// VALU pattern; the 64-bit shift of the doubled word keeps it scalar.)
+__device__ __forceinline__ uint32_t srotr32(uint32_t x, uint32_t n) {
+    return (uint32_t)((((uint64_t)x << 32) | x) >> n);
+}
+__device__ __forceinline__ uint64_t srotr64(uint64_t x, uint32_t n) { return (x >> n) | (x << (64u - n)); }
+
 // 64-bit values as explicit (lo, hi) halves so rotates are v_alignbit pairs.
 struct u64p {
     uint32_t lo, hi;
@@ -237,6 +251,7 @@ struct Md5 {
     static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_MD5;
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
     static constexpr bool kLdsStream = true;  // fixed-stride batches: LDS-DMA line stream
+    static constexpr bool kScalarPad = false;  // no schedule to move: pad block via compress()
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -341,6 +356,7 @@ struct Sha1 {
     static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_SHA1;
     static constexpr bool kPairLoad = true;
     static constexpr bool kLdsStream = true;
+    static constexpr bool kScalarPad = true;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -350,6 +366,17 @@ struct Sha1 {
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(raw[i]);
+        rounds<false>(w);
+    }
+    // Pad-only block (0x80, zeros, BE bit length) from a wave-uniform length:
+    // the schedule is scalar work (see md_pad_only).
+    __device__ __forceinline__ void compress_pad(uint64_t bytes) {
+        uint32_t w[16] = {0x80000000u};
+        w[14] = (uint32_t)(bytes >> 29); w[15] = (uint32_t)(bytes << 3);
+        rounds<true>(w);
+    }
+    template <bool kUniform>  // w: BE words
+    __device__ __forceinline__ void rounds(uint32_t (&w)[16]) {
         uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
 #pragma unroll
         for (int i = 0; i < 80; ++i) {
@@ -357,7 +384,12 @@ struct Sha1 {
             if (i < 16) {
                 x = w[i];
             } else {
-                x = rotl32(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15] ^ w[i & 15]), 1);
+                if (kUniform) {
+                    const uint32_t y = w[(i - 3) & 15] ^ w[(i - 8) & 15] ^ w[(i - 14) & 15] ^ w[i & 15];
+                    x = srotr32(y, 31);
+                } else {
+                    x = rotl32(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15] ^ w[i & 15]), 1);
+                }
                 w[i & 15] = x;
             }
             uint32_t f, k;
@@ -365,7 +397,7 @@ struct Sha1 {
             else if (i < 40) { f = xor3(b, c, d); k = 0x6ed9eba1u; }
             else if (i < 60) { f = maj3(b, c, d); k = 0x8f1bbcdcu; }
             else { f = xor3(b, c, d); k = 0xca62c1d6u; }
-            const uint32_t t = rotl32(a, 5) + f + e + k + x;
+            const uint32_t t = kUniform ? rotl32(a, 5) + f + e + (k + x) : rotl32(a, 5) + f + e + k + x;
             e = d; d = c; c = rotl32(b, 30); b = a; a = t;
         }
         s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e;
@@ -400,6 +432,7 @@ struct Sha256 {
                          kOcc = LCB_OCC_SHA256;
     static constexpr bool kPairLoad = LCB_PAIR_SHA256;  // VALU-bound: fewer live VGPRs
     static constexpr bool kLdsStream = LCB_LDS_SHA256;
+    static constexpr bool kScalarPad = true;
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -414,6 +447,16 @@ struct Sha256 {
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(raw[i]);
+        rounds<false>(w);
+    }
+    // Pad-only block from a wave-uniform length (scalar schedule, md_pad_only).
+    __device__ __forceinline__ void compress_pad(uint64_t bytes) {
+        uint32_t w[16] = {0x80000000u};
+        w[14] = (uint32_t)(bytes >> 29); w[15] = (uint32_t)(bytes << 3);
+        rounds<true>(w);
+    }
+    template <bool kUniform>  // w: BE words
+    __device__ __forceinline__ void rounds(uint32_t (&w)[16]) {
         uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
@@ -422,14 +465,20 @@ struct Sha256 {
                 x = w[i];
             } else {
                 const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-                const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-                const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+                uint32_t s0, s1;
+                if (kUniform) {
+                    s0 = srotr32(w15, 7) ^ srotr32(w15, 18) ^ (w15 >> 3);
+                    s1 = srotr32(w2, 17) ^ srotr32(w2, 19) ^ (w2 >> 10);
+                } else {
+                    s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+                    s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+                }
                 x = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
                 w[i & 15] = x;
             }
             const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
             const uint32_t ch = ch3(e, f, g);
-            const uint32_t t1 = h + S1 + ch + kSha256K[i] + x;
+            const uint32_t t1 = kUniform ? h + S1 + ch + (kSha256K[i] + x) : h + S1 + ch + kSha256K[i] + x;
             const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
             const uint32_t mj = maj3(a, b, c);
             h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
@@ -478,6 +527,7 @@ struct Sha512 {
                          kOcc = LCB_OCC_SHA512;
     static constexpr bool kPairLoad = false;  // 128-B blocks already
     static constexpr bool kLdsStream = LCB_LDS_SHA512;
+    static constexpr bool kScalarPad = true;
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143
@@ -519,6 +569,49 @@ struct Sha512 {
     template <int... I>
     __device__ __forceinline__ static void rounds(Vars& v, std::integer_sequence<int, I...>) {
         (round<I>(v), ...);
+    }
+    // Pad-only block from a wave-uniform length: the 80-word schedule is
+    // computed in plain 64-bit C (scalar ALU) and K[i] + W[i] is folded into
+    // one wave-uniform operand (md_pad_only).
+    struct UVars {
+        uint64_t w[16];
+        u64p a, b, c, d, e, f, g, h;
+    };
+    template <int i>
+    __device__ __forceinline__ static void uround(UVars& v) {
+        uint64_t x;
+        if (i < 16) {
+            x = v.w[i];
+        } else {
+            const uint64_t w15 = v.w[(i - 15) & 15], w2 = v.w[(i - 2) & 15];
+            const uint64_t s0 = srotr64(w15, 1) ^ srotr64(w15, 8) ^ (w15 >> 7);
+            const uint64_t s1 = srotr64(w2, 19) ^ srotr64(w2, 61) ^ (w2 >> 6);
+            x = v.w[i & 15] + s0 + v.w[(i - 7) & 15] + s1;
+            v.w[i & 15] = x;
+        }
+        const u64p S1 = xor3p(rotr64p<14>(v.e), rotr64p<18>(v.e), rotr64p<41>(v.e));
+        const u64p ch = u64p{ch3(v.e.lo, v.f.lo, v.g.lo), ch3(v.e.hi, v.f.hi, v.g.hi)};
+        const uint64_t t1 = add64(add64k(v64(v.h), kSha512Kc[i] + x), add64(v64(S1), v64(ch)));
+        const u64p S0 = xor3p(rotr64p<28>(v.a), rotr64p<34>(v.a), rotr64p<39>(v.a));
+        const u64p mj = u64p{maj3(v.a.lo, v.b.lo, v.c.lo), maj3(v.a.hi, v.b.hi, v.c.hi)};
+        v.h = v.g; v.g = v.f; v.f = v.e; v.e = mk64(add64(v64(v.d), t1)); v.d = v.c; v.c = v.b; v.b = v.a;
+        v.a = mk64(add64(t1, add64(v64(S0), v64(mj))));
+    }
+    template <int... I>
+    __device__ __forceinline__ static void urounds(UVars& v, std::integer_sequence<int, I...>) {
+        (uround<I>(v), ...);
+    }
+    __device__ __forceinline__ void compress_pad(uint64_t bytes) {
+        UVars v;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v.w[i] = 0;
+        v.w[0] = 0x8000000000000000ull;
+        v.w[14] = bytes >> 61; v.w[15] = bytes << 3;
+        v.a = mk64(s[0]); v.b = mk64(s[1]); v.c = mk64(s[2]); v.d = mk64(s[3]);
+        v.e = mk64(s[4]); v.f = mk64(s[5]); v.g = mk64(s[6]); v.h = mk64(s[7]);
+        urounds(v, std::make_integer_sequence<int, 80>{});
+        s[0] += v64(v.a); s[1] += v64(v.b); s[2] += v64(v.c); s[3] += v64(v.d);
+        s[4] += v64(v.e); s[5] += v64(v.f); s[6] += v64(v.g); s[7] += v64(v.h);
     }
     __device__ __forceinline__ void compress(const uint32_t* raw) {
         Vars v;
@@ -650,11 +743,10 @@ struct LdsLineStream {
     }
 };
 
+// Compresses `nfull` whole blocks starting at p; returns the pointer after them.
 template <class H>
-__device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
+__device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p, uint64_t nfull) {
     uint32_t w[H::kWords];
-    const uint64_t nfull = len / H::kBlock;
-    const uint8_t* p = msg;
     uint64_t b = 0;
     if (H::kPairLoad && LCB_PREFETCH) {
         // Two blocks = one 128-B line per step, the next line's loads in
@@ -691,6 +783,14 @@ __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t l
         load_block_full<H>(p, w);
         st.compress(w);
     }
+    return p;
+}
+
+template <class H>
+__device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
+    uint32_t w[H::kWords];
+    const uint64_t nfull = len / H::kBlock;
+    const uint8_t* p = md_full_blocks(st, msg, nfull);
     const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
     load_block_tail<H>(p, rem, w);
     // 0x80 terminator at byte `rem` (of a 64- or 128-byte block).
@@ -704,6 +804,26 @@ __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t l
     }
     H::put_length(w, len + prefix);
     st.compress(w);
+}
+
+// Final block of a message whose length is a whole number of blocks: 0x80,
+// zeros, length (md5.h:271-283, sha1.h:816-834, sha2.h:714-733).  Equal to
+// md_message(st, p, 0, total) but built from `total` alone, so when `total`
+// is wave-uniform (fixed-length batches) the block and the SHA message
+// schedule derived from it live in SGPRs and run on the scalar ALU, leaving
+// the VALU only the rounds.
+template <class H>
+__device__ __forceinline__ void md_pad_only(H& st, uint64_t total) {
+    if constexpr (H::kScalarPad) {
+        st.compress_pad(total);
+    } else {
+        uint32_t w[H::kWords];
+#pragma unroll
+        for (int k = 0; k < H::kWords; ++k) w[k] = 0u;
+        w[0] = 0x80u;
+        H::put_length(w, total);
+        st.compress(w);
+    }
 }
 
 // Outer HMAC pass over an inner digest held in registers (digest words are

@@ -21,6 +21,19 @@ __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint
 }
 
 // ------------------------------------------------------------- MD family
+// Message body: fixed-length batches of whole blocks take the pad-only final
+// block from the kernel-argument length (wave-uniform, scalar schedule).
+template <class H>
+__device__ __forceinline__ void md_body(H& st, const KArgs& a, const uint8_t* msg, uint64_t len,
+                                        uint64_t prefix) {
+    if (LCB_UNIFORM_PAD && !a.lengths && a.fixed_len % H::kBlock == 0) {
+        md_full_blocks(st, msg, (uint64_t)a.fixed_len / H::kBlock);
+        md_pad_only(st, (uint64_t)a.fixed_len + prefix);
+    } else {
+        md_message(st, msg, len, prefix);
+    }
+}
+
 template <class H, bool kHmac>
 __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
     uint64_t idx, len;
@@ -30,7 +43,7 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
     uint32_t dw[H::kDigest / 4];
     if (kHmac) {
         load_words(st.s, a.mid);                       // state after K ^ ipad
-        md_message(st, msg, len, (uint64_t)H::kBlock);
+        md_body(st, a, msg, len, (uint64_t)H::kBlock);
         st.digest_words(dw);
         H o;
         load_words(o.s, a.mid + kMidWords);            // state after K ^ opad
@@ -38,7 +51,7 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
         o.digest_words(dw);
     } else {
         st.init();
-        md_message(st, msg, len, 0);
+        md_body(st, a, msg, len, 0);
         st.digest_words(dw);
     }
     store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
@@ -83,7 +96,11 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     const uint64_t i = wave_first + lane;
     if (i > last) return;
     const uint8_t* msg = a.data + i * a.stride + nlines * 128;
-    md_message(st, msg, (uint64_t)a.fixed_len - nlines * 128, prefix + nlines * 128);
+    const uint64_t tail = (uint64_t)a.fixed_len - nlines * 128;
+    if (LCB_UNIFORM_PAD && tail == 0)  // wave-uniform: schedule of the pad block on the SALU
+        md_pad_only(st, prefix + nlines * 128);
+    else
+        md_message(st, msg, tail, prefix + nlines * 128);
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kHmac) {

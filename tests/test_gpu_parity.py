@@ -147,6 +147,24 @@ def test_every_alignment_and_tail_length(gpu, oracle):
         assert np.array_equal(got.cpu().numpy(), exp), alg
 
 
+@pytest.mark.parametrize("stride_pad", [0, 16, 3])
+def test_fixed_whole_block_lengths(gpu, oracle, stride_pad):
+    """Fixed-length batches whose length is a whole number of blocks end in a
+    pad-only block built from the wave-uniform length (md_pad_only: scalar
+    schedule).  Lengths 0..4096 in 64-B steps x plain/HMAC; stride padding 0
+    and 16 take the LDS line-stream kernel where eligible, 3 the generic one;
+    300 records so the last wave is partial."""
+    n = 300
+    for L in (0, 64, 128, 192, 256, 320, 448, 512, 1024, 1088, 2048, 4096):
+        stride = L + stride_pad
+        data = gen_stream(1000 + L, max(1, n * stride))
+        for alg in range(1, 9):
+            for key in (None, b"k" * 20, bytes(range(200))):
+                exp = oracle.batch(alg, data, count=n, stride=stride, fixed_len=L, key=key)
+                got = gpu.hash_batch(alg, dev(data), count=n, stride=stride, fixed_len=L, key=key)
+                assert np.array_equal(got.cpu().numpy(), exp), (alg, L, stride, key is not None)
+
+
 def test_unaligned_digest_output(gpu, oracle):
     data = gen_stream(1, 64 * 100)
     for alg in (1, 2, 6, 7):
