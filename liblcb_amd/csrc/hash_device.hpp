@@ -62,6 +62,16 @@
 #ifndef LCB_LDS_SHA256
 #define LCB_LDS_SHA256 1
 #endif
+// Half-line (64-B) stages for the fixed-stride kernel (md_fixed_half_kernel).
+#ifndef LCB_HALF_MD5
+#define LCB_HALF_MD5 0
+#endif
+#ifndef LCB_HALF_SHA1
+#define LCB_HALF_SHA1 0
+#endif
+#ifndef LCB_HALF_SHA256
+#define LCB_HALF_SHA256 0
+#endif
 #ifndef LCB_LDS_SHA512
 #define LCB_LDS_SHA512 0
 #endif
@@ -252,6 +262,7 @@ struct Md5 {
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
     static constexpr bool kLdsStream = true;  // fixed-stride batches: LDS-DMA line stream
     static constexpr bool kScalarPad = false;  // no schedule to move: pad block via compress()
+    static constexpr bool kHalfStream = LCB_HALF_MD5;
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -357,6 +368,7 @@ struct Sha1 {
     static constexpr bool kPairLoad = true;
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
+    static constexpr bool kHalfStream = LCB_HALF_SHA1;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -433,6 +445,7 @@ struct Sha256 {
     static constexpr bool kPairLoad = LCB_PAIR_SHA256;  // VALU-bound: fewer live VGPRs
     static constexpr bool kLdsStream = LCB_LDS_SHA256;
     static constexpr bool kScalarPad = true;
+    static constexpr bool kHalfStream = LCB_HALF_SHA256;
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -528,6 +541,7 @@ struct Sha512 {
     static constexpr bool kPairLoad = false;  // 128-B blocks already
     static constexpr bool kLdsStream = LCB_LDS_SHA512;
     static constexpr bool kScalarPad = true;
+    static constexpr bool kHalfStream = false;
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143
@@ -722,26 +736,75 @@ struct LdsLineStream {
             src[g] = data + j * stride + ((lane & 7) ^ f) * 16;
         }
     }
-    __device__ __forceinline__ void issue(uint64_t L) const {
+    // Line L into slab buffer `buf` (8 KiB each; one buffer per line in flight).
+    __device__ __forceinline__ void issue(uint64_t L, uint32_t buf = 0) const {
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + L * 128),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
-                                             LCB_LDS_AUX);
+                                             (__attribute__((address_space(3))) void*)(slab + buf * 8192 + g * 1024),
+                                             16, 0, LCB_LDS_AUX);
     }
-    // Waits for the issued line, copies this lane's 128 B (raw LE words).
-    __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16]) const {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line landed
+    // Waits for the oldest issued line (kLater lines issued after it may stay
+    // in flight: 8 DMA instructions each), copies this lane's 128 B of buffer
+    // `buf` (raw LE words).
+    template <int kLater = 0>
+    __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16], uint32_t buf = 0) const {
+        if (kLater == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (kLater == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         const uint32_t fj = (lane >> 1) & 7;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(slab + lane * 128 + ((k ^ fj) * 16));
+            const uint4 v = *reinterpret_cast<const uint4*>(slab + buf * 8192 + lane * 128 + ((k ^ fj) * 16));
             uint32_t* d = (k < 4) ? (w0 + 4 * k) : (w1 + 4 * (k - 4));
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab free again
     }
 };
+
+// Half-line variant: stage = one 64-B block of each of the wave's 64 records
+// (4 KiB: 4 DMA instructions of 16 records x 64 B), so a wave needs half the
+// LDS per stage in flight.  Slot swizzle: chunk k of local record j sits in
+// slot k ^ ((j >> 2) & 3), conflict-free for 16-lane ds_read_b128 groups.
+struct LdsHalfStream {
+    const uint8_t* src[4];
+    uint8_t* slab;
+    uint32_t lane;
+    __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first,
+                                         uint64_t last, uint32_t ln, uint8_t* my_slab) {
+        lane = ln;
+        slab = my_slab;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // instruction g: local records 16g .. 16g+15
+            uint64_t j = wave_first + 16 * g + (lane >> 2);
+            j = j > last ? last : j;
+            src[g] = data + j * stride + (((lane & 3) ^ ((lane >> 4) & 3)) * 16);
+        }
+    }
+    __device__ __forceinline__ void issue(uint64_t B, uint32_t buf) const {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + B * 64),
+                                             (__attribute__((address_space(3))) void*)(slab + buf * 4096 + g * 1024),
+                                             16, 0, LCB_LDS_AUX);
+    }
+    template <int kLater>
+    __device__ __forceinline__ void take(uint32_t w[16], uint32_t buf) const {
+        if (kLater == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (kLater == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (kLater == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        const uint32_t fj = (lane >> 2) & 3;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = *reinterpret_cast<const uint4*>(slab + buf * 4096 + lane * 64 + ((k ^ fj) * 16));
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+};
+
 
 // Compresses `nfull` whole blocks starting at p; returns the pointer after them.
 template <class H>

@@ -63,11 +63,21 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 // of its 64 records into LDS (LdsLineStream, hash_device.hpp) while the two
 // 64-B blocks of line L are compressed.  Bytes after the last whole line go
 // through the generic loader.
+// LCB_LDS_DEPTH lines in flight per wave (8 KiB of LDS each), LCB_FIXED_WPG
+// waves per workgroup.
+#ifndef LCB_LDS_DEPTH
+#define LCB_LDS_DEPTH 1
+#endif
+#ifndef LCB_FIXED_WPG
+#define LCB_FIXED_WPG 4
+#endif
 template <class H, bool kHmac>
-__global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+__global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_lds_kernel(KArgs a) {
+    constexpr int kDepth = LCB_LDS_DEPTH, kWpg = LCB_FIXED_WPG;
+    static_assert(kDepth >= 1 && kDepth <= 3, "1..3 lines in flight");
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kWpg][kDepth * 8192];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * kWpg + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
     const uint64_t last = a.count - 1;
     const uint64_t nlines = a.fixed_len / 128;
@@ -81,11 +91,32 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     } else {
         st.init();
     }
-    if (nlines) ls.issue(0);
+#ifndef LCB_EXP_SPLIT  // time-split experiments: 1 = no loads, 2 = no compression
+#define LCB_EXP_SPLIT 0
+#endif
+    if (LCB_EXP_SPLIT != 1) {
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d)
+            if ((uint64_t)d < nlines) ls.issue(d, d);
+    }
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
-        ls.take(w, w + 16);              // line L -> VGPRs, slab free again
-        if (L + 1 < nlines) ls.issue(L + 1);
+        if (LCB_EXP_SPLIT == 1) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) w[k] = lane * 0x9e3779b9u + (uint32_t)L * 977u + k;
+        } else {
+            const uint32_t buf = (uint32_t)(L % kDepth);
+            const uint64_t later = nlines - 1 - L;  // lines issued after L (capped by depth)
+            if (kDepth >= 3 && later >= 2) ls.take<2>(w, w + 16, buf);
+            else if (kDepth >= 2 && later >= 1) ls.take<1>(w, w + 16, buf);
+            else ls.take<0>(w, w + 16, buf);  // line L -> VGPRs, its buffer free again
+            if (L + kDepth < nlines) ls.issue(L + kDepth, buf);
+        }
+        if (LCB_EXP_SPLIT == 2) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) st.s[k % (sizeof(st.s) / sizeof(st.s[0]))] ^= w[k];
+            continue;
+        }
         if constexpr (H::kBlock == 128) {
             st.compress(w);              // one SHA-384/512 block per line
         } else {
@@ -101,6 +132,64 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
         md_pad_only(st, prefix + nlines * 128);
     else
         md_message(st, msg, tail, prefix + nlines * 128);
+    uint32_t dw[H::kDigest / 4];
+    st.digest_words(dw);
+    if (kHmac) {
+        H o;
+        load_words(o.s, a.mid + kMidWords);
+        md_outer(o, dw);
+        o.digest_words(dw);
+    }
+    store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
+}
+
+// Half-line stages (LdsHalfStream): one 64-B block of each record per stage,
+// LCB_HALF_DEPTH stages in flight per wave; 64-B-block algorithms only.
+#ifndef LCB_HALF_DEPTH
+#define LCB_HALF_DEPTH 2
+#endif
+template <class H, bool kHmac>
+__global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_half_kernel(KArgs a) {
+    static_assert(H::kBlock == 64, "64-B blocks");
+    constexpr int kDepth = LCB_HALF_DEPTH, kWpg = LCB_FIXED_WPG;
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kWpg][kDepth * 4096];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * kWpg + wv) * 64;
+    if (wave_first >= a.count) return;  // wave-uniform
+    const uint64_t last = a.count - 1;
+    const uint64_t nblk = a.fixed_len / 64;
+    LdsHalfStream ls;
+    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
+    H st;
+    uint64_t prefix = 0;
+    if (kHmac) {
+        load_words(st.s, a.mid);
+        prefix = H::kBlock;
+    } else {
+        st.init();
+    }
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d)
+        if ((uint64_t)d < nblk) ls.issue(d, d);
+    for (uint64_t B = 0; B < nblk; ++B) {
+        uint32_t w[16];
+        const uint32_t buf = (uint32_t)(B % kDepth);
+        const uint64_t later = nblk - 1 - B;
+        if (kDepth >= 4 && later >= 3) ls.take<3>(w, buf);
+        else if (kDepth >= 3 && later >= 2) ls.take<2>(w, buf);
+        else if (kDepth >= 2 && later >= 1) ls.take<1>(w, buf);
+        else ls.take<0>(w, buf);
+        if (B + kDepth < nblk) ls.issue(B + kDepth, buf);
+        st.compress(w);
+    }
+    const uint64_t i = wave_first + lane;
+    if (i > last) return;
+    const uint8_t* msg = a.data + i * a.stride + nblk * 64;
+    const uint64_t tail = (uint64_t)a.fixed_len - nblk * 64;
+    if (LCB_UNIFORM_PAD && tail == 0)
+        md_pad_only(st, prefix + nblk * 64);
+    else
+        md_message(st, msg, tail, prefix + nblk * 64);
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kHmac) {
@@ -335,8 +424,15 @@ template <class H>
 static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
     if constexpr (H::kLdsStream) {
         if (fixed_lds_ok(a)) {
-            if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
+            const dim3 grid((unsigned)((a.count + 64 * LCB_FIXED_WPG - 1) / (64 * LCB_FIXED_WPG)));
+            const dim3 block(64 * LCB_FIXED_WPG);
+            if constexpr (H::kBlock == 64 && H::kHalfStream) {
+                if (hmac) hipLaunchKernelGGL((md_fixed_half_kernel<H, true>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((md_fixed_half_kernel<H, false>), grid, block, 0, s, a);
+                return;
+            }
+            if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid, block, 0, s, a);
             return;
         }
     }
