@@ -91,17 +91,17 @@ def settle(seconds=0.4):
     del scratch
 
 
-def hash_launch(alg, data, digests, count, stream):
-    return lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), None, None, count, MSG_LEN,
-                                MSG_LEN, digests.data_ptr(), F_DEVICE, stream)
+def hash_launch(alg, data, digests, count, stream, key=None):
+    return lib().lcb_hash_batch(alg, key, len(key) if key else 0, data.data_ptr(), None, None, count,
+                                MSG_LEN, MSG_LEN, digests.data_ptr(), F_DEVICE, stream)
 
 
-def time_alg(alg, data, digests, count, steps, warmup, world):
+def time_alg(alg, data, digests, count, steps, warmup, world, key=None):
     """Returns (wall seconds for `steps` passes, max over ranks; mean kernel ms)."""
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for _ in range(warmup):
-        check(hash_launch(alg, data, digests, count, sp))
+        check(hash_launch(alg, data, digests, count, sp, key))
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     torch.cuda.synchronize()
@@ -111,7 +111,7 @@ def time_alg(alg, data, digests, count, steps, warmup, world):
     t0 = time.perf_counter()
     for s, e in ev:
         s.record(stream)
-        check(hash_launch(alg, data, digests, count, sp))
+        check(hash_launch(alg, data, digests, count, sp, key))
         e.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -378,6 +378,19 @@ def main():
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
             del dg
         out["per_alg"] = per
+        # Batched HMAC (RADIUS needs HMAC-MD5): per call
+        # the ipad/opad mid-states are computed on the device (one tiny prep
+        # kernel), then every message costs its blocks + 1 outer compression.
+        hm = {}
+        key = bytes(range(16))
+        for name in ("md5", "sha1", "sha256", "sha512"):
+            aid = ALG_IDS[name]
+            dg = torch.empty((count, DIGEST_SIZE[aid]), dtype=torch.uint8, device="cuda")
+            tt, km = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1, key=key)
+            hm["hmac_" + name] = {"GiB_s": round(count * MSG_LEN * max(3, a.steps // 4) / tt / 2**30, 2),
+                                  "call_ms": round(km, 4), "key_bytes": len(key)}
+            del dg
+        out["hmac"] = hm
         out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
         out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
         settle()   # ChaCha20 is VALU-heavy: let the clock settle after the HBM-bound CRC launches
