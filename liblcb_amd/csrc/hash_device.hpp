@@ -763,6 +763,36 @@ struct LdsLineStream {
     }
 };
 
+// Ragged variant: record j of the wave streams from its own base pointer
+// (any 16-B aligned start), re-reading its last whole line once it runs out
+// (the data is discarded; every DMA stays inside the record).  Bases and
+// limits are exchanged across lanes once, at init.
+struct GatherLineStream : LdsLineStream {
+    uint32_t lim[8];
+    __device__ __forceinline__ void init_gather(const uint8_t* base, uint32_t last_line, uint32_t ln,
+                                                uint8_t* my_slab) {
+        lane = ln;
+        slab = my_slab;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const int j = 8 * g + (int)(ln >> 3);
+            const uint64_t b = __shfl((unsigned long long)reinterpret_cast<uintptr_t>(base), j, 64);
+            lim[g] = (uint32_t)__shfl((int)last_line, j, 64);
+            const uint32_t f = ((ln >> 4) + 4 * g) & 7;
+            src[g] = reinterpret_cast<const uint8_t*>(b) + ((ln & 7) ^ f) * 16;
+        }
+    }
+    __device__ __forceinline__ void issue_clamped(uint32_t L) const {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t l = L < lim[g] ? L : lim[g];
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + (uint64_t)l * 128),
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             LCB_LDS_AUX);
+        }
+    }
+};
+
 // Half-line variant: stage = one 64-B block of each of the wave's 64 records
 // (4 KiB: 4 DMA instructions of 16 records x 64 B), so a wave needs half the
 // LDS per stage in flight.  Slot swizzle: chunk k of local record j sits in

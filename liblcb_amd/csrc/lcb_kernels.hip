@@ -143,6 +143,86 @@ __global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_lds_kernel(KArgs 
     store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
 }
 
+// ------------------------------------------- MD family, ragged LDS-DMA path
+// Ragged batches (offsets and/or lengths, normally bucketed by length so a
+// wave's records have similar block counts): the whole 128-B lines of the
+// wave's 64 records stream through LDS like the fixed-stride path
+// (GatherLineStream), each lane compressing only its own lines; the tail and
+// padding go through the per-lane loader.  A wave whose records do not all
+// start 16-B aligned takes the per-lane path for the whole message.
+// Parity-green but off: on the C4 mix ({64 B, 1 KiB, 64 KiB}) it is 11 %
+// slower for MD5 and within 1 % for SHA-1/SHA-256 (profiles/r1_gather_ab.txt).
+// The 5.3K waves of 64 KiB records outnumber the 5 x 4 LDS-limited wave
+// slots per CU (5,120 chip-wide), so the last ones run alone, where the
+// per-lane kernel (8 waves per SIMD) holds all of them at once.
+#ifndef LCB_GATHER_LDS
+#define LCB_GATHER_LDS 0
+#endif
+template <class H, bool kHmac>
+__global__ __launch_bounds__(256) void md_gather_lds_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    if (wave_first >= a.count) return;  // wave-uniform
+    const uint64_t last = a.count - 1, i = wave_first + lane, ic = i > last ? last : i;
+    const uint64_t idx = a.order ? (uint64_t)gptr(a.order)[ic] : ic;
+    const uint8_t* msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
+    const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
+    H st;
+    uint64_t prefix = 0;
+    if (kHmac) {
+        load_words(st.s, a.mid);
+        prefix = H::kBlock;
+    } else {
+        st.init();
+    }
+    const uint32_t nl = (uint32_t)((len >> 7) < 0xffffffu ? (len >> 7) : 0xffffffu);  // lines streamed
+    const bool ok = nl == 0 || (reinterpret_cast<uintptr_t>(msg) & 15u) == 0;
+    uint64_t done = 0;
+    if (__all(ok)) {  // wave-uniform
+        uint32_t mx = nl;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t v = (uint32_t)__shfl_xor((int)mx, o, 64);
+            mx = v > mx ? v : mx;
+        }
+        if (mx > 0) {
+            const int lead = (int)__builtin_ctzll(__ballot(nl == mx));  // a lane with mx lines
+            const uint64_t lead_msg =
+                __shfl((unsigned long long)reinterpret_cast<uintptr_t>(msg), lead, 64);
+            const uint8_t* base = nl ? msg : reinterpret_cast<const uint8_t*>(lead_msg);
+            GatherLineStream gs;
+            gs.init_gather(base, (nl ? nl : mx) - 1, lane, &slab[wv][0]);
+            gs.issue_clamped(0);
+            for (uint32_t L = 0; L < mx; ++L) {
+                uint32_t w[32];
+                gs.take(w, w + 16);
+                if (L + 1 < mx) gs.issue_clamped(L + 1);
+                if (L < nl) {
+                    if constexpr (H::kBlock == 128) {
+                        st.compress(w);
+                    } else {
+                        st.compress(w);
+                        st.compress(w + 16);
+                    }
+                }
+            }
+            done = (uint64_t)nl * 128;
+        }
+    }
+    if (i > last) return;
+    md_message(st, msg + done, len - done, prefix + done);
+    uint32_t dw[H::kDigest / 4];
+    st.digest_words(dw);
+    if (kHmac) {
+        H o;
+        load_words(o.s, a.mid + kMidWords);
+        md_outer(o, dw);
+        o.digest_words(dw);
+    }
+    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
+}
+
 // Half-line stages (LdsHalfStream): one 64-B block of each record per stage,
 // LCB_HALF_DEPTH stages in flight per wave; 64-B-block algorithms only.
 #ifndef LCB_HALF_DEPTH
@@ -433,6 +513,13 @@ static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
             }
             if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid, block, 0, s, a);
+            return;
+        }
+    }
+    if constexpr (H::kLdsStream) {
+        if (LCB_GATHER_LDS && a.order) {  // bucketed ragged batch
+            if (hmac) hipLaunchKernelGGL((md_gather_lds_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((md_gather_lds_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
             return;
         }
     }

@@ -249,6 +249,34 @@ def test_bucketed_equals_unbucketed(gpu, oracle):
         assert np.array_equal(whole, np.concatenate(parts)), alg
 
 
+@pytest.mark.parametrize("layout", ["aligned16", "packed", "mostly_aligned"])
+def test_ragged_line_stream(gpu, oracle, layout):
+    """Bucketed ragged batches (count above the bucketing threshold) take the
+    LDS line-stream gather kernel (md_gather_lds_kernel): waves whose records
+    all start 16-B aligned stream their whole lines through LDS, the others
+    fall back per wave.  Lengths 0..3000 plus a few 64 KiB records, so waves
+    mix records with and without whole lines; plain and HMAC."""
+    rng = np.random.default_rng(len(layout))
+    n = 6000
+    lens = rng.integers(0, 3001, n).astype(np.uint32)
+    lens[rng.integers(0, n, 40)] = 65536
+    lens[rng.integers(0, n, 40)] = 128 * rng.integers(1, 9, 40)
+    offs = np.zeros(n, np.uint64)
+    pos = 0
+    for k in range(n):
+        if layout == "aligned16" or (layout == "mostly_aligned" and k % 997 != 5):
+            pos = (pos + 15) // 16 * 16
+        offs[k] = pos
+        pos += int(lens[k]) + int(rng.integers(0, 3))
+    data = gen_stream(99, pos + 16)
+    dd, dl, do = dev(data), dev(lens, np.int32), dev(offs, np.int64)
+    for alg in range(1, 7):
+        for key in (None, b"radius-secret"):
+            exp = oracle.batch(alg, data, offs, lens, key=key)
+            got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=key).cpu().numpy()
+            assert np.array_equal(got, exp), (alg, layout, key is not None)
+
+
 def test_host_mode_pinned_direct_dma(gpu, batches):
     """Host mode from page-locked input (direct DMA, rebased offsets for ragged
     chunks) and from pageable input (parallel gather), multi-chunk sizes."""
