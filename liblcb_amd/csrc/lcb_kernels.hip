@@ -71,6 +71,9 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 #ifndef LCB_FIXED_WPG
 #define LCB_FIXED_WPG 4
 #endif
+#ifndef LCB_DMA_PRIO
+#define LCB_DMA_PRIO 0
+#endif
 template <class H, bool kHmac>
 __global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_lds_kernel(KArgs a) {
     constexpr int kDepth = LCB_LDS_DEPTH, kWpg = LCB_FIXED_WPG;
@@ -107,10 +110,12 @@ __global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_lds_kernel(KArgs 
         } else {
             const uint32_t buf = (uint32_t)(L % kDepth);
             const uint64_t later = nlines - 1 - L;  // lines issued after L (capped by depth)
+            if (LCB_DMA_PRIO) __builtin_amdgcn_s_setprio(3);  // take + re-issue ahead of other waves' VALU
             if (kDepth >= 3 && later >= 2) ls.take<2>(w, w + 16, buf);
             else if (kDepth >= 2 && later >= 1) ls.take<1>(w, w + 16, buf);
             else ls.take<0>(w, w + 16, buf);  // line L -> VGPRs, its buffer free again
             if (L + kDepth < nlines) ls.issue(L + kDepth, buf);
+            if (LCB_DMA_PRIO) __builtin_amdgcn_s_setprio(0);
         }
         if (LCB_EXP_SPLIT == 2) {
 #pragma unroll
