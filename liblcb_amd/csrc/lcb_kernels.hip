@@ -74,8 +74,15 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 #ifndef LCB_DMA_PRIO
 #define LCB_DMA_PRIO 0
 #endif
+// LCB_FIXED_OCC: pass the algorithm's occupancy target (capped at the 5
+// waves per SIMD the LDS allows) as the kernel's waves-per-SIMD bound.
+#ifndef LCB_FIXED_OCC
+#define LCB_FIXED_OCC 0
+#endif
+template <class H>
+constexpr int fixed_occ() { return LCB_FIXED_OCC ? (H::kOcc < 5 ? H::kOcc : 5) : 1; }
 template <class H, bool kHmac>
-__global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_lds_kernel(KArgs a) {
+__global__ __launch_bounds__(64 * LCB_FIXED_WPG, fixed_occ<H>()) void md_fixed_lds_kernel(KArgs a) {
     constexpr int kDepth = LCB_LDS_DEPTH, kWpg = LCB_FIXED_WPG;
     static_assert(kDepth >= 1 && kDepth <= 3, "1..3 lines in flight");
     __shared__ __attribute__((aligned(16))) uint8_t slab[kWpg][kDepth * 8192];
