@@ -2,19 +2,36 @@
 """Benchmark: device-resident GiB/s hashed, 1M x 1 KiB buffers per MI355X.
 
 One step = one pass of the batch digest kernel over the rank's shard of
-1,048,576 x 1,024-byte buffers (BASELINE.json configs[2]; at --gpus 8 the 8
-shards form configs[4], 8M x 1 KiB).  Inputs are generated on the device by
-the synthetic-stream kernel before timing (no host traffic in the timed
-region).  Shards are independent (weak scaling, no data-path collective);
-the only collectives are the barrier and the max-over-ranks of the time.
+the global batch of 1,024-byte buffers.  Inputs are generated on the device
+by the synthetic-stream kernel before timing (no host traffic in the timed
+region).  Shards are independent (no data-path collective); the only
+collectives in the timed region are the barrier and the max-over-ranks of
+the time.
+
+  --scaling weak    (default) 1,048,576 buffers per GPU (BASELINE configs[2]);
+                    at --gpus 8 the union is configs[4], 8M x 1 KiB
+  --scaling strong  a fixed global batch (--global-count, default 8M x 1 KiB
+                    = configs[4]) split over the N GPUs
+
+Shards come from lcb_hash_partition (include/lcb_hash_gpu.h), the library's
+own work-balanced split.  `--gpus N` without a torch.distributed launcher
+starts the N ranks itself (a torch.distributed.run child, before any GPU
+call); under a launcher WORLD_SIZE must equal N.  After timing, the ranks'
+digests are gathered to rank 0 over RCCL (timed separately, never part of
+`value`) and checked against the reference's digest-of-digests
+(tests/golden/batches.json C3, tests/golden/large.json C5).
 
 Extra fields on the JSON line:
   roofline      dominant kernel vs HBM peak (algorithmic bytes / HIP-event
                 kernel time); traffic from a committed rocprofv3 PMC summary
-                (profiles/pmc_<alg>.json) when one exists for this workload
+                (profiles/pmc_<alg>.json) when one exists for this workload;
+                valu_frac = VALU issue floor (committed SQ_INSTS_VALU count,
+                profiles/valu_counts.json, x 4 cycles on 1,024 SIMDs at
+                2.4 GHz) / kernel time
   cpu_baseline  the reference's own include/crypto code (oracle/_ref, built
                 from /root/reference) timed on this host's cores, rank 0, N=1
-  per_alg       the same measurement for every algorithm (N=1)
+  per_alg       the same measurement for every algorithm (N=1), each with
+                hbm_frac, valu_frac and the reference CPU rate beside it
   e2e           host-memory path: pinned input -> H2D -> kernel -> D2H
   crc32/chacha  the CRC-32 family and ChaCha/XChaCha over the same bytes
   verify        GPU digests of the timed workload vs the CPU reference run
@@ -45,24 +62,59 @@ CPU_SAMPLE_S = 1.0  # wall seconds of the CPU baseline sample (x threads of CPU 
 MSGS_PER_GPU = 1 << 20
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--alg", default="md5", choices=sorted(ALG_IDS))
-    p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU")
+    p.add_argument("--scaling", default="weak", choices=("weak", "strong"))
+    p.add_argument("--count", type=int, default=MSGS_PER_GPU, help="buffers per GPU (weak scaling)")
+    p.add_argument("--global-count", type=int, default=8 * MSGS_PER_GPU,
+                   help="buffers of the whole job (strong scaling)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     p.add_argument("--no-extras", action="store_true", help="skip per_alg / e2e")
+    p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather + fixture check")
     p.add_argument("--cpu-threads", type=int, default=0)
-    return p.parse_args()
+    p.add_argument("--plan", action="store_true",
+                   help="print every rank's shard (gloo, no GPU use) and exit: launch-path check")
+    return p.parse_args(argv)
 
 
-def shard_bounds(rank, world, per_gpu):
-    """Weak scaling: rank r owns buffers [r*per_gpu, (r+1)*per_gpu) of the
-    global batch, i.e. bytes starting at r*per_gpu*MSG_LEN of the stream."""
+def spawn_ranks(a, argv):
+    """`--gpus N` run directly: start N ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process, before this process touches the
+    GPU, and exit with its status."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def global_count(scaling, world, per_gpu, global_count_strong):
+    return per_gpu * world if scaling == "weak" else global_count_strong
+
+
+def shard_bounds(rank, world, per_gpu, scaling="weak", global_count_strong=None):
+    """(first buffer, buffers) of rank r: lcb_hash_partition of the global
+    batch into `world` work-balanced contiguous parts.  Weak scaling: the
+    global batch is world x per_gpu (rank r owns [r*per_gpu, (r+1)*per_gpu));
+    strong: a fixed global_count_strong buffers."""
     assert 0 <= rank < world
-    return rank * per_gpu, per_gpu
+    total = global_count(scaling, world, per_gpu, global_count_strong)
+    first = liblcb_amd.partition(world, count=total, fixed_len=MSG_LEN)
+    return int(first[rank]), int(first[rank + 1] - first[rank])
 
 
 def max_over_ranks(t, world):
@@ -138,6 +190,56 @@ def pmc_traffic(alg, count):
         return None
 
 
+VALU_CYCLES = 4.0        # cycles per wave64 VALU instruction in a mixed stream
+VALU_SIMDS = 1024        # 256 CUs x 4 SIMDs
+VALU_CLOCK_HZ = 2.4e9    # MI355X max engine clock (MI355X_MICROARCH.md)
+
+
+def valu_floor_ms(alg, count):
+    """VALU issue floor of one launch on the bench workload: the committed
+    SQ_INSTS_VALU count (profiles/valu_counts.json, rocprofv3 --pmc) x 4
+    cycles / (1,024 SIMDs x 2.4 GHz).  None without a count for this shape."""
+    path = os.path.join(ROOT, "profiles", "valu_counts.json")
+    try:
+        j = json.load(open(path))
+        if j.get("count") != count or j.get("msg_len") != MSG_LEN:
+            return None
+        n = float(j["algs"][ALG_NAMES[alg]]["SQ_INSTS_VALU"])
+    except (OSError, ValueError, KeyError):
+        return None
+    return n * VALU_CYCLES / (VALU_SIMDS * VALU_CLOCK_HZ) * 1e3
+
+
+def host_threads():
+    """Threads the CPU baseline uses: the CPUs this process may run on."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cgroup_cpus():
+    """CPU quota of this container (cgroup v2 cpu.max), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _ref_rate(r, alg, data, count, threads, min_s):
+    """GiB/s of the reference over the first `count` buffers, repeated until
+    `min_s` wall seconds; returns (rate, seconds, digests, reps)."""
+    r.batch_fixed_mt(alg, data[:MSG_LEN * 256], 256, MSG_LEN, MSG_LEN, threads=threads)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        d = r.batch_fixed_mt(alg, data, count, MSG_LEN, MSG_LEN, threads=threads)
+        reps += 1
+        t = time.perf_counter() - t0
+        if t >= min_s:
+            return reps * count * MSG_LEN / t / 2**30, t, d, reps
+
+
 def cpu_baseline(alg, count, threads):
     """The reference's include/crypto path (oracle/_ref, compiled from the
     reference headers) on this host's cores, over the same 1M x 1 KiB bytes.
@@ -148,18 +250,7 @@ def cpu_baseline(alg, count, threads):
     res = {}
     for kind, path in (("reference", REF_SO), ("reference-simd", REF_SIMD_SO)):
         if os.path.exists(path):
-            r = Ref(path)
-            r.batch_fixed_mt(alg, data[:MSG_LEN * 1024], 1024, MSG_LEN, MSG_LEN, threads=threads)
-            # Repeat the whole workload until >= CPU_SAMPLE_S of wall time
-            # (threads x that of CPU work), report the mean rate.
-            reps, t0 = 0, time.perf_counter()
-            while True:
-                d = r.batch_fixed_mt(alg, data, count, MSG_LEN, MSG_LEN, threads=threads)
-                reps += 1
-                t = time.perf_counter() - t0
-                if t >= CPU_SAMPLE_S:
-                    break
-            res[kind] = (reps * count * MSG_LEN / t / 2**30, t, d, reps)
+            res[kind] = _ref_rate(Ref(path), alg, data, count, threads, CPU_SAMPLE_S)
     if not res:
         o = Oracle()
         t0 = time.perf_counter()
@@ -167,16 +258,33 @@ def cpu_baseline(alg, count, threads):
         t = time.perf_counter() - t0
         res["port"] = (count * MSG_LEN / t / 2**30, t, d, 1)
     best = max(res, key=lambda k: res[k][0])
-    # Single-thread rate of the best build on a bounded sample (~1 s).
-    one = None
     path = {"reference": REF_SO, "reference-simd": REF_SIMD_SO}.get(best)
+    one = t16 = None
     if path:
         r = Ref(path)
         n1 = min(count, 1 << 18)
-        t0 = time.perf_counter()
-        r.batch_fixed_mt(alg, data[:n1 * MSG_LEN], n1, MSG_LEN, MSG_LEN, threads=1)
-        one = n1 * MSG_LEN / (time.perf_counter() - t0) / 2**30
-    return best, res, one
+        one = _ref_rate(r, alg, data, n1, 1, 0.0)[0]               # one pass, one thread
+        if threads != 16:
+            t16 = _ref_rate(r, alg, data, count, 16, 0.5)[0]       # the box's nominal CPU share
+    return best, res, one, t16, data
+
+
+def cpu_per_alg(data, threads, best):
+    """Reference CPU rate of every algorithm on a bounded sample of the same
+    bytes (about 0.3 s wall each), the build `best` picked for the headline."""
+    from oracle.pyoracle import REF_SIMD_SO, REF_SO, Ref
+    path = {"reference": REF_SO, "reference-simd": REF_SIMD_SO}.get(best)
+    if not path or not os.path.exists(path):
+        return {}
+    r = Ref(path)
+    out = {}
+    for name, aid in sorted(ALG_IDS.items(), key=lambda x: x[1]):
+        n = 1 << 14
+        rate, t, _, _ = _ref_rate(r, aid, data, n, threads, 0.0)
+        n = int(min(len(data) // MSG_LEN, max(n, n * 0.3 / max(t, 1e-6))))   # ~0.3 s
+        rate, t, _, _ = _ref_rate(r, aid, data, n, threads, 0.0)
+        out[name] = {"GiB_s": round(rate, 3), "buffers": n, "threads": threads, "seconds": round(t, 3)}
+    return out
 
 
 def cpu_model():
@@ -187,6 +295,45 @@ def cpu_model():
     except OSError:
         pass
     return None
+
+
+def fixture_dod(alg, total):
+    """Reference digest-of-digests for the global fixed-stride batch of
+    `total` x 1 KiB buffers (seed SEED), or None if no fixture covers it."""
+    name = ALG_NAMES[alg]
+    if total == MSGS_PER_GPU:
+        b = json.load(open(os.path.join(ROOT, "tests", "golden", "batches.json")))
+        for e in b["batches"]:
+            if e["name"] == "C3_1M_x_1k" and e["alg"] == name and "key" not in e:
+                return e["dod"]
+    if total == 8 * MSGS_PER_GPU:
+        j = json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))
+        return j["C5_8M_x_1k"]["algs"][name]["dod"]
+    return None
+
+
+def gather_digests(digests, first, n, total, world, rank):
+    """RCCL gather of every rank's digests to rank 0; the
+    shards are padded to the largest.  Returns (host array on rank 0, ms)."""
+    D = digests.shape[1]
+    if world == 1:
+        torch.cuda.synchronize()
+        return digests.cpu().numpy(), 0.0
+    first_all = liblcb_amd.partition(world, count=total, fixed_len=MSG_LEN)
+    mx = int(np.max(np.diff(first_all.astype(np.int64))))
+    buf = torch.zeros((mx, D), dtype=torch.uint8, device="cuda")
+    buf[:n] = digests
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    dist.gather(buf, parts, dst=0)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    if rank != 0:
+        return None, ms
+    out = [parts[r][:int(first_all[r + 1] - first_all[r])] for r in range(world)]
+    return torch.cat(out).cpu().numpy(), ms
 
 
 def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
@@ -216,9 +363,18 @@ def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
         launch()
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / steps
+    ab = total + count * (D + 12)          # bytes read once + digest + (u64 offset, u32 length)
     res = {"GiB_s": round(total / t / 2**30, 2), "ms_per_pass": round(t * 1e3, 3),
            "total_GiB": round(total / 2**30, 2), "buffers": count,
+           "hbm_frac": round(ab / t / 1e9 / HBM_PEAK_GBS, 4),
            "lengths": "{64, 1024, 65536}[mix64(seed+i) % 3]", "bucketed": True}
+    try:
+        j = json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))["C4_1M_mixed"]
+        if j["count"] == count and j["total_bytes"] == total:
+            res["dod_equals_reference"] = hashlib.sha256(dig.cpu().numpy().tobytes()).hexdigest() == \
+                j["algs"][ALG_NAMES[alg]]["dod"]
+    except (OSError, KeyError, ValueError):
+        pass
     del data, dig
     torch.cuda.empty_cache()
     return res
@@ -317,54 +473,100 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
             "path": "producer memcpy into pinned lease -> H2D -> kernel -> D2H -> per-packet callback"}
 
 
+def plan(a, world, rank):
+    """--plan: the launch and sharding path without the GPU (gloo): every
+    rank reports its shard, rank 0 prints them as one JSON line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == a.gpus
+    first, count = shard_bounds(rank, world, a.count, a.scaling, a.global_count)
+    me = {"rank": rank, "world_size": dist.get_world_size() if world > 1 else 1, "first": first,
+          "count": count, "pid": os.getpid()}
+    allp = [None] * world
+    if world > 1:
+        dist.all_gather_object(allp, me)
+        dist.destroy_process_group()
+    else:
+        allp = [me]
+    if rank == 0:
+        print(json.dumps({"plan": allp, "scaling": a.scaling,
+                          "total": global_count(a.scaling, world, a.count, a.global_count)}), flush=True)
+    return 0
+
+
 def main():
-    a = parse()
+    argv = sys.argv[1:]
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
+    if a.plan:
+        return plan(a, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     else:
         torch.cuda.set_device(0)
     alg = ALG_IDS[a.alg]
-    count = a.count
     D = DIGEST_SIZE[alg]
 
-    # Rank r hashes buffers [r*count, (r+1)*count) of the global synthetic batch.
-    first, count = shard_bounds(rank, world, count)
-    data = liblcb_amd.gen_synthetic(SEED, count * MSG_LEN, start=first * MSG_LEN)
-    digests = torch.empty((count, D), dtype=torch.uint8, device="cuda")
+    # Rank r hashes its lcb_hash_partition shard of the global synthetic batch.
+    total = global_count(a.scaling, world, a.count, a.global_count)
+    first, count = shard_bounds(rank, world, a.count, a.scaling, a.global_count)
+    data = liblcb_amd.gen_synthetic(SEED, max(count, 1) * MSG_LEN, start=first * MSG_LEN)
+    digests = torch.empty((max(count, 1), D), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
 
     settle()
     t, kms = time_alg(alg, data, digests, count, a.steps, a.warmup, world)
-    total_bytes = world * count * MSG_LEN * a.steps
-    value = total_bytes / t / 2**30
+    value = total * MSG_LEN * a.steps / t / 2**30
     alg_bytes = count * (MSG_LEN + D)      # read every message once + write its digest
     achieved = alg_bytes / (kms * 1e-3) / 1e9
     traffic = pmc_traffic(alg, count)
+    vfloor = valu_floor_ms(alg, count)
     out = {
         "metric": "device-resident GiB/s hashed, 1M x 1 KiB buffers per GPU",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
+        "world_size": dist.get_world_size() if world > 1 else 1,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(t / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "u32" if alg not in (5, 6, 7, 8) else "u64",
         "data": "synthetic (device-generated splitmix64 stream, SURVEY.md 8d)",
-        "config": {"workload": "%s digest of %d x %d B buffers per GPU" % (a.alg, count, MSG_LEN),
+        "config": {"workload": "%s digest of %d x %d B buffers over %d GPU(s), %s scaling"
+                               % (a.alg, total, MSG_LEN, world, a.scaling),
                    "alg": a.alg, "buffers_per_gpu": count, "buffer_bytes": MSG_LEN,
-                   "total_buffers": world * count, "parallelism": "shard%d" % world},
+                   "total_buffers": total, "parallelism": "shard%d" % world,
+                   "split": "lcb_hash_partition (work-balanced contiguous shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kms, 4),
-                     "algorithmic_bytes_per_launch": alg_bytes},
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "valu_floor_ms": round(vfloor, 4) if vfloor else None,
+                     "valu_frac": round(vfloor / kms, 4) if vfloor else None},
     }
+
+    if not a.no_gather:
+        # RCCL digest gather to rank 0 (outside the timed region), then the
+        # whole job's digests against the reference's digest-of-digests.
+        allg, gms = gather_digests(digests[:count], first, count, total, world, rank)
+        if rank == 0:
+            exp = fixture_dod(alg, total)
+            got = hashlib.sha256(allg.tobytes()).hexdigest()
+            out["gather"] = {"ms": round(gms, 3), "bytes": int(allg.nbytes), "collective": "gather (RCCL)"
+                             if world > 1 else "none (1 rank)"}
+            out.setdefault("verify", {})["job_digests_equal_reference"] = (got == exp) if exp else None
+            out["verify"]["digest_of_digests"] = got
 
     if rank == 0 and world == 1 and not a.no_extras:
         settle()
@@ -373,9 +575,11 @@ def main():
             dg = torch.empty((count, DIGEST_SIZE[aid]), dtype=torch.uint8, device="cuda")
             tt, km = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1)
             ab = count * (MSG_LEN + DIGEST_SIZE[aid])
+            vf = valu_floor_ms(aid, count)
             per[name] = {"GiB_s": round(count * MSG_LEN * max(3, a.steps // 4) / tt / 2**30, 2),
                          "kernel_ms": round(km, 4),
-                         "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                         "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "valu_frac": round(vf / km, 4) if vf else None}
             del dg
         out["per_alg"] = per
         # Batched HMAC (RADIUS needs HMAC-MD5): per call
@@ -415,33 +619,41 @@ def main():
         out["e2e"] = e2e
         torch.cuda.synchronize()
         gpu_dig = digests.cpu().numpy()
-        out["verify"] = {"e2e_equals_device": bool(np.array_equal(hd, gpu_dig))}
+        out.setdefault("verify", {})["e2e_equals_device"] = bool(np.array_equal(hd, gpu_dig))
 
     if rank == 0 and world == 1 and not a.no_cpu:
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        best, res, one = cpu_baseline(alg, count, threads)
+        threads = a.cpu_threads or host_threads()
+        best, res, one, t16, cdata = cpu_baseline(alg, count, threads)
         gbs, tcpu, dcpu, reps = res[best]
-        gpu_dig = digests.cpu().numpy()
+        gpu_dig = digests[:count].cpu().numpy()
         out["cpu_baseline"] = {
             "value": round(gbs, 3), "unit": "GiB/s", "cores": threads, "kind": "reference"
             if best.startswith("reference") else "port",
-            "build": best, "sample": "the full workload (%d x %d B, %s) hashed %d times on %d threads, "
-            "one contiguous shard per thread, %.1f s wall" % (count, MSG_LEN, a.alg, reps, threads, tcpu),
+            "build": best, "sample": "the full workload (%d x %d B, %s) hashed %d times on %d threads "
+            "(sched_getaffinity), one contiguous shard per thread, %.1f s wall"
+            % (count, MSG_LEN, a.alg, reps, threads, tcpu),
             "all": {k: round(v[0], 3) for k, v in res.items()},
             "one_thread": round(one, 3) if one else None,
+            "at_16_threads": round(t16, 3) if t16 else None,
+            "cgroup_cpus": cgroup_cpus(),
             "cpu_model": cpu_model(),
             "build_flags": {"reference": "gcc -O2 -fPIC, #undef __SSE2__ (as tests/hash/main.c:36)",
                             "reference-simd": "gcc -O2 -fPIC -msse4.1 -mssse3 -msha -mavx2 (cpuid dispatch)"},
             "seconds": round(tcpu, 3)}
+        cpa = cpu_per_alg(cdata, threads, best)
+        for name, v in cpa.items():
+            if name in out.get("per_alg", {}):
+                out["per_alg"][name]["cpu_GiB_s"] = v["GiB_s"]
+        out["cpu_baseline"]["per_alg"] = cpa
         out.setdefault("verify", {})["gpu_equals_cpu_reference"] = bool(np.array_equal(gpu_dig, dcpu))
-        out["verify"]["digest_of_digests"] = hashlib.sha256(gpu_dig.tobytes()).hexdigest()
 
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define LCB_HASH_GPU_ABI_VERSION	1
+#define LCB_HASH_GPU_ABI_VERSION	2
 
 /* Algorithm ids. */
 #define LCB_HASH_MD5		1	/* md5.h */
@@ -62,6 +62,10 @@ extern "C" {
 
 /* Flags. */
 #define LCB_HASH_F_DEVICE	0x0001u
+/* lcb_hash_batch_multi, device mode, diagnostics: parts 1..ndev-1 take the
+ * peer-copy path even when they run on devs[0] (a same-device copy), so one
+ * GPU exercises the scatter/gather code. */
+#define LCB_HASH_F_COPY_PARTS	0x0100u
 
 /* Information. */
 int	lcb_hash_gpu_abi_version(void);
@@ -131,6 +135,31 @@ int	gost3411_2012_hmac_get_digest_batch(size_t bits, const uint8_t *key,
 	    const uint32_t *lengths, size_t count, uint64_t stride,
 	    uint32_t fixed_len, uint8_t *digests, size_t *digest_size,
 	    uint32_t flags, void *stream);
+
+/* Multi-device batches. ---------------------------------
+ *
+ * lcb_hash_partition: cut a batch into `nparts` contiguous message ranges of
+ * balanced work (message bytes + one 64-B padding block each; lengths NULL:
+ * equal counts).  Part p = messages [first[p], first[p+1]); `first` holds
+ * nparts + 1 entries, lengths are HOST memory.  The bench's one-process-per-
+ * GPU mode shards with the same rule.
+ *
+ * lcb_hash_batch_multi: lcb_hash_batch with the batch split by
+ * lcb_hash_partition over devs[0..ndev-1] (HIP device ordinals; repeats
+ * allowed), all parts concurrently; returns when every digest is written.
+ *   flags 0                 host memory, one staging pipeline per part;
+ *   flags LCB_HASH_F_DEVICE data/offsets/lengths/digests are device memory on
+ *                           devs[0]; a part on another device is copied peer-
+ *                           to-peer (xGMI), hashed there, and its digests are
+ *                           copied back into `digests` on devs[0].
+ * With devs = {d} it equals lcb_hash_batch on device d.  Errors: EINVAL,
+ * ENODEV (an ordinal out of range), ENOMEM, EIO. */
+int	lcb_hash_partition(const uint32_t *lengths, size_t count,
+	    uint32_t fixed_len, size_t nparts, uint64_t *first);
+int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
+	    const uint8_t *key, size_t key_len, const uint8_t *data,
+	    const uint64_t *offsets, const uint32_t *lengths, size_t count,
+	    uint64_t stride, uint32_t fixed_len, uint8_t *digests, uint32_t flags);
 
 /* Synthetic input: writes bytes [start, start+n) of the stream
  * whose u64 word k (little-endian) is mix64(seed ^ k), into device memory. */

@@ -26,6 +26,7 @@ DIGEST_SIZE = {MD5: 16, SHA1: 20, SHA224: 28, SHA256: 32, SHA384: 48, SHA512: 64
                GOST256: 32, GOST512: 64}
 BLOCK_SIZE = {a: (128 if a in (SHA384, SHA512) else 64) for a in DIGEST_SIZE}
 F_DEVICE = 0x1
+F_COPY_PARTS = 0x100
 
 _lib = None
 
@@ -56,6 +57,9 @@ SIGNATURES = [
      [c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
     ("gost3411_2012_hmac_get_digest_batch", ctypes.c_int,
      [c_sz, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("lcb_hash_partition", ctypes.c_int, [c_vp, c_sz, c_u32, c_sz, c_vp]),
+    ("lcb_hash_batch_multi", ctypes.c_int,
+     [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32]),
     ("lcb_hash_gen_synthetic", ctypes.c_int, [c_u64, c_u64, c_vp, c_sz, c_vp]),
     ("lcb_hash_gpu_gost_table", ctypes.c_int, [c_vp]),
 ]

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from ._lib import F_DEVICE, check, lib
-from .hash import _is_dev, _layout
+from .hash import _check_extent, _is_dev, _layout
 
 __all__ = ["chacha_batch", "xchacha_batch"]
 
@@ -49,8 +49,11 @@ def _crypt(x, key, src, dst, key_size, counters, ivs, rounds, offsets, lengths, 
             assert src.dtype == torch.uint8 and src.is_contiguous()
         counters = _dev_u8(counters, 8, count, "counters")
         ivs = _dev_u8(ivs, ivl, count, "ivs")
+        _check_extent(total, count, offsets, lengths, stride, fixed_len)
         if dst is None:
             dst = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+        assert dst.dtype == torch.uint8 and dst.is_contiguous() and dst.device == dev
+        _check_extent(dst.numel(), count, offsets, lengths, stride, fixed_len)
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev).cuda_stream
             check(L.lcb_chacha_batch(1 if x else 0, kbuf, key_size,
@@ -74,15 +77,19 @@ def _crypt(x, key, src, dst, key_size, counters, ivs, rounds, offsets, lengths, 
     if lengths is not None:
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
     count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, total)
+    _check_extent(total, count, offsets, lengths, stride, fixed_len)
     if dst is None:
         dst = np.zeros(max(total, 1), dtype=np.uint8)
     assert dst.dtype == np.uint8 and dst.flags.c_contiguous
+    _check_extent(dst.size, count, offsets, lengths, stride, fixed_len)
     if counters is not None:
         counters = np.ascontiguousarray(np.frombuffer(bytes(counters), np.uint8)
                                         if isinstance(counters, (bytes, bytearray)) else counters, dtype=np.uint8)
     if ivs is not None:
         ivs = np.ascontiguousarray(np.frombuffer(bytes(ivs), np.uint8)
                                    if isinstance(ivs, (bytes, bytearray)) else ivs, dtype=np.uint8)
+    assert counters is None or counters.size >= 8 * count, "counters"
+    assert ivs is None or ivs.size >= ivl * count, "ivs"
     check(L.lcb_chacha_batch(1 if x else 0, kbuf, key_size,
                              counters.ctypes.data if counters is not None else None,
                              ivs.ctypes.data if ivs is not None else None, rounds,

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ._lib import F_DEVICE, check, lib
-from .hash import _is_dev, _layout
+from .hash import _check_extent, _is_dev, _layout
 
 CRC32A, CRC32CKSUM, CRC32MPEG2, CRC32B, CRC32JAMCRC, CRC32C, CRC32D, CRC32Q = range(1, 9)
 CRC_NAMES = {CRC32A: "crc32a", CRC32CKSUM: "crc32cksum", CRC32MPEG2: "crc32mpeg2",
@@ -35,8 +35,12 @@ def crc32_batch(variant, data, *, offsets=None, lengths=None, count=None, stride
                       (init, (torch.int32, torch.uint32))):
             if t is not None:
                 assert _is_dev(t) and t.dtype in dt and t.is_contiguous() and t.device == data.device
+        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
+        if init is not None:
+            assert init.numel() >= count
         if out is None:
             out = torch.empty(count, dtype=torch.int32, device=data.device)
+        assert out.numel() >= count
         with torch.cuda.device(data.device):
             stream = torch.cuda.current_stream(data.device).cuda_stream
             check(L.lcb_crc32_batch(variant, init.data_ptr() if init is not None else None,
@@ -48,6 +52,7 @@ def crc32_batch(variant, data, *, offsets=None, lengths=None, count=None, stride
     if isinstance(data, (bytes, bytearray, memoryview)):
         data = np.frombuffer(bytes(data), dtype=np.uint8)
     data = np.ascontiguousarray(data, dtype=np.uint8)
+    nbytes = data.size
     if data.size == 0:
         data = np.zeros(1, dtype=np.uint8)
     if offsets is not None:
@@ -57,8 +62,12 @@ def crc32_batch(variant, data, *, offsets=None, lengths=None, count=None, stride
     if init is not None:
         init = np.ascontiguousarray(init, dtype=np.uint32)
     count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
+    if init is not None:
+        assert init.size >= count
     if out is None:
         out = np.empty(count, dtype=np.uint32)
+    assert out.dtype == np.uint32 and out.flags.c_contiguous and out.size >= count
     check(L.lcb_crc32_batch(variant, init.ctypes.data if init is not None else None, data.ctypes.data,
                             offsets.ctypes.data if offsets is not None else None,
                             lengths.ctypes.data if lengths is not None else None,

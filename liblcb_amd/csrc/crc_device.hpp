@@ -112,47 +112,6 @@ struct CrcRule {
     }
 };
 
-// Slicing-by-4 over a LANE-PRIVATE LDS image (crc_priv_kernel): table k,
-// entry b sits once per bank, at byte (k >> 1) * 64 KiB + b * 256 +
-// (k & 1) * 128 + bank * 4, and lane l always reads bank l & 31 — so every
-// ds_read_b32 of a 32-lane group touches 32 distinct banks, conflict-free
-// for any data (the compact 8-table form meets ~3.5 entries on its busiest
-// bank, ~7 LDS cycles per instruction instead of 2).  A lookup address is ONE
-// v_perm_b32: message byte -> bits 8-15, the lane's (k & 1, bank) offset ->
-// bits 0-7, k >> 1 -> bit 16.  128 KiB: one 1024-thread workgroup per CU.
-template <bool kRefl>
-struct CrcRulePriv {
-    __attribute__((address_space(3))) const uint8_t* L;
-    uint32_t base[4];
-    __device__ __forceinline__ void init(__attribute__((address_space(3))) const uint8_t* lds) {
-        L = lds;
-        const uint32_t l = threadIdx.x & 31u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) base[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (l << 2);
-    }
-    // Table k at byte bi of src.
-    __device__ __forceinline__ uint32_t at(int k, uint32_t src, int bi) const {
-        const uint32_t a = __builtin_amdgcn_perm(src, base[k], 0x0c020000u | ((4u + (uint32_t)bi) << 8));
-        return *reinterpret_cast<__attribute__((address_space(3))) const uint32_t*>(L + a);
-    }
-    __device__ __forceinline__ uint32_t step4(uint32_t r, uint32_t w) const {
-        if (kRefl) {
-            const uint32_t x = r ^ w;
-            return xor3(at(3, x, 0), at(2, x, 1), at(1, x, 2)) ^ at(0, x, 3);
-        } else {
-            const uint32_t x = r ^ bswap32(w);
-            return xor3(at(3, x, 3), at(2, x, 2), at(1, x, 1)) ^ at(0, x, 0);
-        }
-    }
-    __device__ __forceinline__ uint32_t step8(uint32_t r, uint32_t w0, uint32_t w1) const {
-        return step4(step4(r, w0), w1);
-    }
-    __device__ __forceinline__ uint32_t step1(uint32_t r, uint32_t b) const {
-        if (kRefl) return (r >> 8) ^ at(0, r ^ b, 0);
-        return (r << 8) ^ at(0, (r >> 24) ^ b, 0);
-    }
-};
-
 // Register value after the whole message (before the variant's output ~).
 template <class Rule>
 __device__ __forceinline__ uint32_t crc_message(const Rule& R, uint32_t r, const uint8_t* msg, uint64_t len) {

@@ -3,14 +3,13 @@
 // Grid as the digest kernels: one lane per buffer, 256-thread workgroups,
 // optional length-bucketing permutation.  The variant's slicing-by-8 tables
 // (8 KiB) are staged into LDS; every lookup is a ds_read_b32 at a
-// data-dependent address, so that kernel is bound by LDS bank conflicts.
-// The default crc_priv_kernel (slicing-by-4, lane-private banks) removes the
-// conflicts and streams at the HBM rate.
+// data-dependent address.  Fixed-stride batches of whole 128-B lines take the
+// LDS-DMA line stream (crc_fixed_lds_kernel), everything else the per-lane
+// kernel; both run at about the HBM rate on 1 KiB buffers.
 #include <hip/hip_runtime.h>
 #include "crc_device.hpp"
 #include "lcb_internal.hpp"
 
-#include <algorithm>
 
 namespace lcbgpu {
 
@@ -28,35 +27,6 @@ __global__ __launch_bounds__(256) void crc_batch_kernel(KArgs a) {
     CrcRule<Var::kRefl> R{T};
     uint32_t r = crc_message(R, Var::kInv ? ~c : c, msg, len);
     gptr(reinterpret_cast<uint32_t*>(a.digests))[idx] = Var::kInv ? ~r : r;
-}
-
-// Persistent lane-private-table kernel (crc_device.hpp CrcRulePriv): one
-// 1024-thread workgroup per CU stages the variant's 4 tables x 32 banks
-// (128 KiB) once and grid-strides over the buffers.
-template <int V>
-__global__ __launch_bounds__(1024) void crc_priv_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t L[32768];
-    using Var = CrcVar<V>;
-    const uint32_t* src = &kCrcTabDev[Var::kFam].t[0][0];
-    uint4* L4 = reinterpret_cast<uint4*>(L);
-    for (uint32_t i = threadIdx.x; i < 8192; i += blockDim.x) {  // 4 banks of one entry per uint4
-        const uint32_t w = i * 4, rem = w & 16383u, d = rem & 63u;
-        const uint32_t k = 2u * (w >> 14) + (d >> 5), b = rem >> 6;
-        const uint32_t v = src[k * 256 + b];
-        L4[i] = make_uint4(v, v, v, v);
-    }
-    __syncthreads();
-    CrcRulePriv<Var::kRefl> R;
-    R.init((__attribute__((address_space(3))) const uint8_t*)L);
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count; i += step) {
-        const uint64_t idx = a.order ? (uint64_t)gptr(a.order)[i] : i;
-        const uint8_t* msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
-        const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
-        const uint32_t c = a.init ? gptr(a.init)[idx] : Var::kOneshot;
-        const uint32_t r = crc_message(R, Var::kInv ? ~c : c, msg, len);
-        gptr(reinterpret_cast<uint32_t*>(a.digests))[idx] = Var::kInv ? ~r : r;
-    }
 }
 
 // Fixed-stride batches (lcb_internal.hpp fixed_stride_lines): the 128-B lines
@@ -93,26 +63,13 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     gptr(reinterpret_cast<uint32_t*>(a.digests))[i] = Var::kInv ? ~r : r;
 }
 
-#ifndef LCB_CRC_FIXED_LDS
-#define LCB_CRC_FIXED_LDS 1
-#endif
-#ifndef LCB_CRC_PRIV
-#define LCB_CRC_PRIV 0
-#endif
-
 template <int V>
 static void launch_crc_v(const KArgs& a, hipStream_t s) {
-#if LCB_CRC_PRIV
-    uint64_t grid = std::min<uint64_t>((uint64_t)device_cu_count(), (a.count + 1023) / 1024);
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(crc_priv_kernel<V>, dim3((unsigned)grid), dim3(1024), 0, s, a);
-#else
     const uint64_t blocks = (a.count + 255) / 256;
-    if (LCB_CRC_FIXED_LDS && fixed_stride_lines(a))
+    if (fixed_stride_lines(a))
         hipLaunchKernelGGL(crc_fixed_lds_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(crc_batch_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
-#endif
 }
 
 void launch_crc(int variant, const KArgs& a, hipStream_t s) {

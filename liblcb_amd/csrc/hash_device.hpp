@@ -20,84 +20,6 @@
 
 #include <utility>
 
-// Occupancy targets (waves per SIMD) per algorithm, used as the second
-// __launch_bounds__ argument; overridable at build time for tuning runs.
-#ifndef LCB_OCC_MD5
-#define LCB_OCC_MD5 8
-#endif
-#ifndef LCB_OCC_SHA1
-#define LCB_OCC_SHA1 8
-#endif
-#ifndef LCB_OCC_SHA256
-#define LCB_OCC_SHA256 4
-#endif
-#ifndef LCB_OCC_SHA512
-#define LCB_OCC_SHA512 4
-#endif
-// LDS-DMA staged fixed-stride kernel (lcb_kernels.hip) for MD5/SHA-1: with
-// the default cache policy it measured equal to direct 128-B line loads; with
-// the nt policy on the DMA stream (LCB_LDS_AUX = 2, lcb_kernels.hip) it is
-// 1.6 % faster on MD5 and SHA-1 (two A/B sessions, back-to-back launches,
-// profiles/r1_md5_variants_ab.txt), so it is the fixed-stride path.
-#ifndef LCB_FIXED_LDS
-#define LCB_FIXED_LDS 1
-#endif
-// Register ping-pong prefetch of the next 128-B line in md_message: at the
-// 8-wave VGPR cap it spills (303 VGPRs to scratch, 3.5x slower); at a 4-wave
-// cap it fits (116 VGPRs) and is 3 % slower than no prefetch.  Off.
-#ifndef LCB_PREFETCH
-#define LCB_PREFETCH 0
-#endif
-// Fixed-length batches whose length is a whole number of blocks end in a
-// pad-only block built from the (wave-uniform) length: md_pad_only.
-#ifndef LCB_UNIFORM_PAD
-#define LCB_UNIFORM_PAD 1
-#endif
-#ifndef LCB_PAIR_SHA256
-#define LCB_PAIR_SHA256 0
-#endif
-// LDS-DMA line stream for fixed-stride SHA-224/256 and SHA-384/512 batches:
-// A/B (profiles/r1_sha2_lds_ab.txt) SHA-224/256 2.4 % faster (on), SHA-384/512
-// 2.5-4 % slower (3 waves/SIMD at 139 VGPRs instead of 4; off).
-#ifndef LCB_LDS_SHA256
-#define LCB_LDS_SHA256 1
-#endif
-// Half-line (64-B) stages for the fixed-stride kernel (md_fixed_half_kernel).
-#ifndef LCB_HALF_MD5
-#define LCB_HALF_MD5 0
-#endif
-#ifndef LCB_HALF_SHA1
-#define LCB_HALF_SHA1 0
-#endif
-#ifndef LCB_HALF_SHA256
-#define LCB_HALF_SHA256 0
-#endif
-#ifndef LCB_LDS_SHA512
-#define LCB_LDS_SHA512 0
-#endif
-// GOST batch kernels: lane-rotated bank-sliced LPS image (gost_device.hpp)
-// instead of the flat 16 KiB table.
-#ifndef LCB_GOST_ROT
-#define LCB_GOST_ROT 1
-#endif
-// Non-temporal (nt) policy on the once-read message stream (A/B knob).
-#ifndef LCB_NT
-#define LCB_NT 0
-#endif
-__device__ __forceinline__ uint4 stream_load16(const uint4* p) {
-#if LCB_NT
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-#define LCB_STREAM_LOAD(p) stream_load16(p)
-#ifndef LCB_OCC_GOST
-#define LCB_OCC_GOST 2
-#endif
-
 namespace lcbgpu {
 
 // ------------------------------------------------------------ primitives
@@ -216,7 +138,7 @@ __device__ __forceinline__ void load_full128(const uint8_t* p, uint32_t w0[16], 
         const uint4* q = reinterpret_cast<const uint4*>(p);
         uint4 v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = LCB_STREAM_LOAD(&q[k]);
+        for (int k = 0; k < 8; ++k) v[k] = q[k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             w0[4 * k + 0] = v[k].x; w0[4 * k + 1] = v[k].y; w0[4 * k + 2] = v[k].z; w0[4 * k + 3] = v[k].w;
@@ -258,11 +180,15 @@ __device__ __forceinline__ void put_byte(uint32_t w[16], uint32_t pos, uint32_t 
 // ================================================================== MD5
 // md5.h:137-229.  Round functions in their bitop3-friendly forms.
 struct Md5 {
-    static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_MD5;
+    // kOcc: waves per SIMD (second __launch_bounds__ argument of the
+    // per-lane kernel).  kPairLoad: read whole 128-B lines (both halves
+    // requested together).  kLdsStream: fixed-stride batches take the LDS-DMA
+    // line stream.  kScalarPad: the pad-only block's schedule runs on the
+    // SALU (md_pad_only).
+    static constexpr int kBlock = 64, kDigest = 16, kLenBytes = 8, kWords = 16, kOcc = 8;
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
-    static constexpr bool kLdsStream = true;  // fixed-stride batches: LDS-DMA line stream
+    static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = false;  // no schedule to move: pad block via compress()
-    static constexpr bool kHalfStream = LCB_HALF_MD5;
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -364,11 +290,10 @@ struct Md5 {
 // ================================================================ SHA-1
 // sha1.h:220-292 with a 16-word rolling schedule.
 struct Sha1 {
-    static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16, kOcc = LCB_OCC_SHA1;
+    static constexpr int kBlock = 64, kDigest = 20, kLenBytes = 8, kWords = 16, kOcc = 8;
     static constexpr bool kPairLoad = true;
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
-    static constexpr bool kHalfStream = LCB_HALF_SHA1;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -440,12 +365,11 @@ __constant__ static const uint32_t kSha256K[64] = {
 
 template <bool k224>
 struct Sha256 {
-    static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16,
-                         kOcc = LCB_OCC_SHA256;
-    static constexpr bool kPairLoad = LCB_PAIR_SHA256;  // VALU-bound: fewer live VGPRs
-    static constexpr bool kLdsStream = LCB_LDS_SHA256;
+    static constexpr int kBlock = 64, kDigest = k224 ? 28 : 32, kLenBytes = 8, kWords = 16, kOcc = 4;
+    static constexpr bool kPairLoad = false;  // VALU-bound: fewer live VGPRs
+    // Line stream on: 2.4 % faster than direct loads (profiles/r1_sha2_lds_ab.txt).
+    static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
-    static constexpr bool kHalfStream = LCB_HALF_SHA256;
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -536,12 +460,12 @@ constexpr uint64_t kSha512Kc[80] = {
 
 template <bool k384>
 struct Sha512 {
-    static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32,
-                         kOcc = LCB_OCC_SHA512;
+    static constexpr int kBlock = 128, kDigest = k384 ? 48 : 64, kLenBytes = 16, kWords = 32, kOcc = 4;
     static constexpr bool kPairLoad = false;  // 128-B blocks already
-    static constexpr bool kLdsStream = LCB_LDS_SHA512;
+    // Line stream off: 2.5-4 % slower (3 waves per SIMD at 139 VGPRs instead
+    // of 4; profiles/r1_sha2_lds_ab.txt, profiles/r1_fixed_occ_ab.txt).
+    static constexpr bool kLdsStream = false;
     static constexpr bool kScalarPad = true;
-    static constexpr bool kHalfStream = false;
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143
@@ -714,10 +638,8 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // k ^ ((j >> 1) & 7)) so the 16-lane ds_read_b128 groups are conflict-free.
 // Lanes beyond the last record load the last record (clamped) and must not
 // store.  The DMA stream carries the nt cache policy (every byte is read
-// once; LCB_LDS_AUX).
-#ifndef LCB_LDS_AUX
-#define LCB_LDS_AUX 2
-#endif
+// once; kLdsAux).
+constexpr int kLdsAux = 2;  // cache policy of the LDS-DMA stream: nt (every byte is read once)
 struct LdsLineStream {
     const uint8_t* src[8];
     uint8_t* slab;
@@ -742,16 +664,12 @@ struct LdsLineStream {
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + L * 128),
                                              (__attribute__((address_space(3))) void*)(slab + buf * 8192 + g * 1024),
-                                             16, 0, LCB_LDS_AUX);
+                                             16, 0, kLdsAux);
     }
-    // Waits for the oldest issued line (kLater lines issued after it may stay
-    // in flight: 8 DMA instructions each), copies this lane's 128 B of buffer
-    // `buf` (raw LE words).
-    template <int kLater = 0>
+    // Waits for the issued line, copies this lane's 128 B of buffer `buf`
+    // (raw LE words); the buffer is free again on return.
     __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16], uint32_t buf = 0) const {
-        if (kLater == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (kLater == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t fj = (lane >> 1) & 7;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -788,83 +706,17 @@ struct GatherLineStream : LdsLineStream {
             const uint32_t l = L < lim[g] ? L : lim[g];
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + (uint64_t)l * 128),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
-                                             LCB_LDS_AUX);
+                                             kLdsAux);
         }
     }
 };
-
-// Half-line variant: stage = one 64-B block of each of the wave's 64 records
-// (4 KiB: 4 DMA instructions of 16 records x 64 B), so a wave needs half the
-// LDS per stage in flight.  Slot swizzle: chunk k of local record j sits in
-// slot k ^ ((j >> 2) & 3), conflict-free for 16-lane ds_read_b128 groups.
-struct LdsHalfStream {
-    const uint8_t* src[4];
-    uint8_t* slab;
-    uint32_t lane;
-    __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first,
-                                         uint64_t last, uint32_t ln, uint8_t* my_slab) {
-        lane = ln;
-        slab = my_slab;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {  // instruction g: local records 16g .. 16g+15
-            uint64_t j = wave_first + 16 * g + (lane >> 2);
-            j = j > last ? last : j;
-            src[g] = data + j * stride + (((lane & 3) ^ ((lane >> 4) & 3)) * 16);
-        }
-    }
-    __device__ __forceinline__ void issue(uint64_t B, uint32_t buf) const {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + B * 64),
-                                             (__attribute__((address_space(3))) void*)(slab + buf * 4096 + g * 1024),
-                                             16, 0, LCB_LDS_AUX);
-    }
-    template <int kLater>
-    __device__ __forceinline__ void take(uint32_t w[16], uint32_t buf) const {
-        if (kLater == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (kLater == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (kLater == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        const uint32_t fj = (lane >> 2) & 3;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(slab + buf * 4096 + lane * 64 + ((k ^ fj) * 16));
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-};
-
 
 // Compresses `nfull` whole blocks starting at p; returns the pointer after them.
 template <class H>
 __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p, uint64_t nfull) {
     uint32_t w[H::kWords];
     uint64_t b = 0;
-    if (H::kPairLoad && LCB_PREFETCH) {
-        // Two blocks = one 128-B line per step, the next line's loads in
-        // flight while the current one is compressed (ping-pong buffers).
-        const uint64_t npair = nfull / 2;
-        if (npair > 0) {
-            uint32_t a0[16], a1[16], b0[16], b1[16];
-            load_full128(p, a0, a1);
-            uint64_t k = 0;
-            for (; k + 2 <= npair; k += 2, p += 256) {
-                load_full128(p + 128, b0, b1);
-                st.compress(a0);
-                st.compress(a1);
-                if (k + 2 < npair) load_full128(p + 256, a0, a1);
-                st.compress(b0);
-                st.compress(b1);
-            }
-            if (k < npair) {
-                st.compress(a0);
-                st.compress(a1);
-                p += 128;
-            }
-            b = 2 * npair;
-        }
-    } else if (H::kPairLoad) {  // two blocks = one 128-B line per iteration
+    if (H::kPairLoad) {  // two blocks = one 128-B line per iteration
         uint32_t w1[16];
         for (; b + 2 <= nfull; b += 2, p += 128) {
             load_full128(p, w, w1);

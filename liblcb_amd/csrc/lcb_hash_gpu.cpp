@@ -80,6 +80,8 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
 // (stream-ordered temporaries, no synchronisation).
 int launch_ordered(int alg, KArgs a, hipStream_t s) {
     uint32_t* work = nullptr;
+    // The bucketing permutation holds message indices as uint32.
+    if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
         const size_t bytes = (kLenClasses + a.count) * sizeof(uint32_t);
         LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&work), bytes, s));
@@ -148,13 +150,11 @@ void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
 
 }  // namespace lcbgpu
 
-using namespace lcbgpu;
-
-namespace {
+namespace lcbgpu {
 
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init = nullptr) {
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init) {
     KArgs a;
     a.data = data; a.offsets = offsets; a.lengths = lengths; a.order = nullptr;
     a.count = count; a.stride = stride; a.fixed_len = fixed_len; a.digests = digests;
@@ -248,11 +248,32 @@ thread_local Stage g_stage;
 constexpr size_t kChunkBytes = 64ull << 20;   // 64 MiB per in-flight chunk
 constexpr size_t kChunkMsgs = 1u << 18;       // 256 K messages per chunk
 
+// Staging contexts for worker threads of the multi-device path: a pool per
+// device, so repeated lcb_hash_batch_multi calls reuse their pinned buffers.
+std::mutex g_pool_m;
+std::vector<Stage*> g_pool;
+
+Stage* stage_acquire(int dev) {
+    std::lock_guard<std::mutex> lk(g_pool_m);
+    for (size_t k = 0; k < g_pool.size(); ++k)
+        if (g_pool[k]->device == dev) {
+            Stage* st = g_pool[k];
+            g_pool.erase(g_pool.begin() + k);
+            return st;
+        }
+    return new Stage();
+}
+void stage_release(Stage* st) {
+    std::lock_guard<std::mutex> lk(g_pool_m);
+    g_pool.push_back(st);
+}
+
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-               uint32_t fixed_len, uint8_t* digests, const uint32_t* init = nullptr) {
+               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage) {
     int dev = 0;
     LCB_TRY(hipGetDevice(&dev));
+    Stage& S = stage ? *stage : g_stage;
     const size_t D = dsize(alg);
     const bool fixed = (offsets == nullptr && lengths == nullptr);
     auto off_of = [&](size_t i) -> uint64_t { return offsets ? offsets[i] : (uint64_t)i * stride; };
@@ -264,9 +285,8 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
         maxlen = 0;
         for (size_t i = 0; i < count; ++i) maxlen = std::max<uint64_t>(maxlen, lengths[i]);
     }
-    int rc = g_stage.ensure(dev, std::max<size_t>(kChunkBytes, maxlen), kChunkMsgs);
+    int rc = S.ensure(dev, std::max<size_t>(kChunkBytes, maxlen), kChunkMsgs);
     if (rc) return rc;
-    Stage& S = g_stage;
     const bool src_pinned = is_pinned(data);
     const bool dig_pinned = is_pinned(digests);
 
@@ -296,7 +316,12 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
         size_t j = i;
         uint64_t base = 0, span = 0, total = 0;
         if (fixed) {
-            const size_t per = stride ? std::max<size_t>(1, (S.cap - fixed_len) / stride + 1) : S.mcap;
+            // Direct DMA copies the span [i*stride, (j-1)*stride + fixed_len);
+            // the gather path packs (j-i) * fixed_len bytes.  Both must fit
+            // one staging buffer (stride < fixed_len, e.g. 0 or overlapping
+            // records, makes the packed size the larger one).
+            size_t per = stride ? std::max<size_t>(1, (S.cap - fixed_len) / stride + 1) : S.mcap;
+            if (!src_pinned) per = std::min<size_t>(per, fixed_len ? S.cap / fixed_len : S.mcap);
             j = std::min(count, i + std::min(per, S.mcap));
             base = (uint64_t)i * stride;
             span = (uint64_t)(j - i - 1) * stride + fixed_len;
@@ -383,7 +408,9 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     return rc3;
 }
 
-}  // namespace
+}  // namespace lcbgpu
+
+using namespace lcbgpu;
 
 // ================================================================== ABI
 extern "C" {
@@ -422,8 +449,9 @@ int lcb_hash_batch(int alg, const uint8_t* key, size_t key_len, const uint8_t* d
     if (int rc = ensure_init()) return rc;
     if (flags & LCB_HASH_F_DEVICE)
         return batch_device(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len,
-                            digests, reinterpret_cast<hipStream_t>(stream));
-    return batch_host(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len, digests);
+                            digests, reinterpret_cast<hipStream_t>(stream), nullptr);
+    return batch_host(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len, digests,
+                      nullptr, nullptr);
 }
 
 int md5_get_digest_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
@@ -542,7 +570,7 @@ int lcb_crc32_batch(int variant, const uint32_t* init, const uint8_t* data, cons
     if (flags & LCB_HASH_F_DEVICE)
         return batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, out,
                             reinterpret_cast<hipStream_t>(stream), init);
-    return batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, out, init);
+    return batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, out, init, nullptr);
 }
 
 #define LCB_CRC_ENTRY(name, id)                                                                       \

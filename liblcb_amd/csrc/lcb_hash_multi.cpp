@@ -1,0 +1,240 @@
+// lcb_hash_multi.cpp — one batch over several MI355X devices
+// (include/lcb_hash_gpu.h: lcb_hash_partition, lcb_hash_batch_multi).
+//
+// every buffer is independent, so a batch shards with no
+// data-path collective.  The batch is cut into contiguous message ranges
+// balanced by compression work (message bytes + one padding block each) at
+// the k/N quantiles of the prefix sum; part p runs on devs[p].
+//
+//   host mode    one worker thread per part, each running the host pipeline
+//                (pinned staging, H2D -> kernel -> D2H) on its device from a
+//                pooled staging context; digests land in the caller's array.
+//   device mode  the batch lives on devs[0].  Parts on devs[0] hash in place;
+//                a part on another device is copied peer-to-peer over xGMI
+//                (hipMemcpyPeerAsync: its byte span, and its rebased offsets),
+//                hashed there, and its digests are copied back next to the
+//                others on devs[0] — the scatter/gather of SURVEY 8(e) as
+//                point-to-point DMA on each link, no collective.
+#include <errno.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/lcb_hash_gpu.h"
+#include "lcb_internal.hpp"
+
+using namespace lcbgpu;
+
+namespace {
+
+// Work of message i: its bytes plus one 64-B block (every message ends in a
+// padding compression, so empty messages are not free).
+constexpr uint64_t kMsgOverhead = 64;
+
+void partition(const uint32_t* lengths, size_t count, uint32_t fixed_len, size_t nparts, uint64_t* first) {
+    first[0] = 0;
+    first[nparts] = count;
+    if (!lengths) {  // equal work per message: equal counts
+        for (size_t p = 1; p < nparts; ++p) first[p] = (uint64_t)((unsigned __int128)count * p / nparts);
+        return;
+    }
+    uint64_t total = 0;
+    for (size_t i = 0; i < count; ++i) total += (uint64_t)lengths[i] + kMsgOverhead;
+    // first[p] = the first message whose work prefix reaches p/nparts of the total.
+    uint64_t acc = 0;
+    size_t i = 0;
+    for (size_t p = 1; p < nparts; ++p) {
+        const uint64_t target = (uint64_t)((unsigned __int128)total * p / nparts);
+        while (i < count && acc + ((uint64_t)lengths[i] + kMsgOverhead) / 2 < target) {
+            acc += (uint64_t)lengths[i] + kMsgOverhead;
+            ++i;
+        }
+        first[p] = i;
+    }
+}
+
+struct Part {
+    int dev;
+    uint64_t lo, hi;
+    int rc = 0;
+};
+
+int multi_host(const std::vector<Part>& parts_in, int alg, const uint8_t* key, size_t key_len,
+               const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, uint64_t stride,
+               uint32_t fixed_len, uint8_t* digests) {
+    std::vector<Part> parts = parts_in;
+    const size_t D = dsize(alg);
+    auto run = [&](Part& p) {
+        if (p.hi <= p.lo) return;
+        if (hipSetDevice(p.dev) != hipSuccess) { p.rc = ENODEV; return; }
+        Stage* st = stage_acquire(p.dev);
+        // Without offsets message lo + k starts at data + (lo + k) * stride.
+        p.rc = batch_host(alg, key, key_len, offsets ? data : data + p.lo * stride,
+                          offsets ? offsets + p.lo : nullptr, lengths ? lengths + p.lo : nullptr,
+                          p.hi - p.lo, stride, fixed_len, digests + p.lo * D, nullptr, st);
+        stage_release(st);
+    };
+    if (parts.size() == 1) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        run(parts[0]);
+        (void)hipSetDevice(cur);
+    } else {
+        std::vector<std::thread> th;
+        for (Part& p : parts) th.emplace_back(run, std::ref(p));
+        for (auto& t : th) t.join();
+    }
+    for (const Part& p : parts)
+        if (p.rc) return p.rc;
+    return 0;
+}
+
+// Per-part device resources of the device-mode path.
+struct DevPart {
+    hipStream_t s = nullptr;
+    uint8_t* data = nullptr;   // peer copy of the part's byte span (remote parts)
+    uint64_t* off = nullptr;
+    uint32_t* len = nullptr;
+    uint8_t* dig = nullptr;
+};
+
+int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, size_t key_len,
+                 const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, uint64_t stride,
+                 uint32_t fixed_len, uint8_t* digests, const std::vector<uint64_t>& h_off,
+                 const std::vector<uint32_t>& h_len, bool copy_all) {
+    const size_t D = dsize(alg);
+    const int home = parts[0].dev;
+    std::vector<DevPart> dp(parts.size());
+    int rc = 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    auto fail = [&](hipError_t e) { if (!rc && e != hipSuccess) rc = map_err(e); return e != hipSuccess; };
+    for (size_t k = 0; k < parts.size() && !rc; ++k) {
+        const Part& p = parts[k];
+        if (p.hi <= p.lo) continue;
+        const uint64_t n = p.hi - p.lo;
+        DevPart& q = dp[k];
+        if (fail(hipSetDevice(p.dev)) || fail(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking))) break;
+        if (p.dev == home && !(copy_all && k > 0)) {  // in place on the home device
+            rc = batch_device(alg, key, key_len, offsets ? data : data + p.lo * stride,
+                              offsets ? offsets + p.lo : nullptr, lengths ? lengths + p.lo : nullptr, n,
+                              stride, fixed_len, digests + p.lo * D, q.s, nullptr);
+            continue;
+        }
+        // Remote part: its byte span [base, end) of the home buffer.
+        uint64_t base, end;
+        std::vector<uint64_t> roff;
+        if (offsets || lengths) {
+            base = UINT64_MAX; end = 0;
+            for (uint64_t i = p.lo; i < p.hi; ++i) {
+                const uint64_t o = offsets ? h_off[i] : i * stride, l = lengths ? h_len[i] : fixed_len;
+                base = std::min(base, o);
+                end = std::max(end, o + l);
+            }
+            roff.resize(n);
+            for (uint64_t i = p.lo; i < p.hi; ++i) roff[i - p.lo] = (offsets ? h_off[i] : i * stride) - base;
+        } else {
+            base = p.lo * stride;
+            end = (p.hi - 1) * stride + fixed_len;
+        }
+        const uint64_t span = end > base ? end - base : 0;
+        if (fail(hipMalloc(reinterpret_cast<void**>(&q.data), std::max<uint64_t>(span, 1))) ||
+            fail(hipMalloc(reinterpret_cast<void**>(&q.dig), n * D)))
+            break;
+        if (span && fail(hipMemcpyPeerAsync(q.data, p.dev, data + base, home, span, q.s))) break;
+        if (offsets || lengths) {
+            if (fail(hipMalloc(reinterpret_cast<void**>(&q.off), n * 8)) ||
+                fail(hipMalloc(reinterpret_cast<void**>(&q.len), n * 4)) ||
+                fail(hipMemcpyAsync(q.off, roff.data(), n * 8, hipMemcpyHostToDevice, q.s)))
+                break;
+            std::vector<uint32_t> rl(n);
+            for (uint64_t i = 0; i < n; ++i) rl[i] = lengths ? h_len[p.lo + i] : fixed_len;
+            if (fail(hipMemcpyAsync(q.len, rl.data(), n * 4, hipMemcpyHostToDevice, q.s)) ||
+                fail(hipStreamSynchronize(q.s)))  // roff / rl are stack temporaries
+                break;
+            rc = batch_device(alg, key, key_len, q.data, q.off, q.len, n, 0, 0, q.dig, q.s, nullptr);
+        } else {
+            rc = batch_device(alg, key, key_len, q.data, nullptr, nullptr, n, stride, fixed_len, q.dig, q.s,
+                              nullptr);
+        }
+        if (!rc) fail(hipMemcpyPeerAsync(digests + p.lo * D, home, q.dig, p.dev, n * D, q.s));
+    }
+    for (size_t k = 0; k < parts.size(); ++k) {
+        DevPart& q = dp[k];
+        if (!q.s) continue;
+        (void)hipSetDevice(parts[k].dev);
+        fail(hipStreamSynchronize(q.s));
+        if (q.data) (void)hipFree(q.data);
+        if (q.off) (void)hipFree(q.off);
+        if (q.len) (void)hipFree(q.len);
+        if (q.dig) (void)hipFree(q.dig);
+        (void)hipStreamDestroy(q.s);
+    }
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lcb_hash_partition(const uint32_t* lengths, size_t count, uint32_t fixed_len, size_t nparts,
+                       uint64_t* first) {
+    if (nparts == 0 || !first) return EINVAL;
+    partition(lengths, count, fixed_len, nparts, first);
+    return 0;
+}
+
+int lcb_hash_batch_multi(const int* devs, int ndev, int alg, const uint8_t* key, size_t key_len,
+                         const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, size_t count,
+                         uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags) {
+    if (!devs || ndev <= 0 || ndev > 64) return EINVAL;
+    if (alg < LCB_HASH_MD5 || alg > LCB_HASH_GOST512) return EINVAL;
+    if (flags & ~(LCB_HASH_F_DEVICE | LCB_HASH_F_COPY_PARTS)) return EINVAL;
+    if (count == 0) return 0;
+    if (!data || !digests) return EINVAL;
+    if (key == nullptr && key_len != 0) return EINVAL;
+    if (int rc = ensure_init()) return rc;
+    int ndevices = 0;
+    if (hipGetDeviceCount(&ndevices) != hipSuccess) return ENODEV;
+    for (int k = 0; k < ndev; ++k)
+        if (devs[k] < 0 || devs[k] >= ndevices) return ENODEV;
+    const bool dev_mode = flags & LCB_HASH_F_DEVICE;
+    // Device mode: the partition (and the remote parts' rebasing) needs the
+    // offsets / lengths on the host.
+    std::vector<uint64_t> h_off;
+    std::vector<uint32_t> h_len;
+    const uint32_t* plen = lengths;
+    if (dev_mode && (offsets || lengths)) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (hipSetDevice(devs[0]) != hipSuccess) return ENODEV;
+        hipError_t e = hipSuccess;
+        if (offsets) {
+            h_off.resize(count);
+            e = hipMemcpy(h_off.data(), offsets, count * 8, hipMemcpyDeviceToHost);
+        }
+        if (e == hipSuccess && lengths) {
+            h_len.resize(count);
+            e = hipMemcpy(h_len.data(), lengths, count * 4, hipMemcpyDeviceToHost);
+        }
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) return map_err(e);
+        plen = lengths ? h_len.data() : nullptr;
+    }
+    std::vector<uint64_t> first(ndev + 1);
+    partition(plen, count, fixed_len, (size_t)ndev, first.data());
+    std::vector<Part> parts(ndev);
+    for (int k = 0; k < ndev; ++k) parts[k] = Part{devs[k], first[k], first[k + 1]};
+    if (dev_mode)
+        return multi_device(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests,
+                            h_off, h_len, flags & LCB_HASH_F_COPY_PARTS);
+    return multi_host(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests);
+}
+
+}  // extern "C"

@@ -8,7 +8,7 @@
 //              indices and a run of arena bytes with one CAS on the slot's
 //              state word [sealed:1 | count:23 | bytes:40], then fills it
 //              packet by packet without writing shared cache lines: per packet
-//              it raises/lowers its lease record's `busy` flag around the copy
+//              it raises/lowers its lease record's `busy` count around the copy
 //              (a Dekker handshake with the flusher's seal) and publishes
 //              `done` (packets written).  Indices a lease did not fill become
 //              holes: zero-length entries that nobody waits for.
@@ -69,7 +69,11 @@ struct Meta {
 };
 
 struct alignas(64) LeaseRec {
-    std::atomic<uint32_t> busy{0};   // producer is between its seal check and publish
+    // Producers between their seal check and publish.  A COUNTER, not a flag:
+    // a producer still holding a lease of an older generation of this slot
+    // announces itself here too (then sees the gen mismatch and leaves), and
+    // must not clear the announcement of the record's current owner.
+    std::atomic<uint32_t> busy{0};
     std::atomic<uint32_t> done{0};   // packets written into this lease
 };
 
@@ -519,7 +523,7 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
             Slot* b = L.slot;
             LeaseRec& r = b->leases[L.rec];
             // Dekker with the flusher: announce, then check the seal.
-            r.busy.store(1, std::memory_order_relaxed);
+            r.busy.fetch_add(1, std::memory_order_relaxed);
             std::atomic_thread_fence(std::memory_order_seq_cst);
             const bool live = b->gen.load(std::memory_order_relaxed) == L.gen &&
                               !b->closed.load(std::memory_order_relaxed);
@@ -538,7 +542,7 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
                 L.idx = i + 1;
                 L.pos = pos + len;
                 r.done.store((uint32_t)(L.idx - (uint64_t)L.rec * LM), std::memory_order_release);
-                r.busy.store(0, std::memory_order_release);
+                r.busy.fetch_sub(1, std::memory_order_release);
                 if (b->t_first.load(std::memory_order_relaxed) == 0) {
                     int64_t z = 0;
                     if (b->t_first.compare_exchange_strong(z, now_ns(), std::memory_order_acq_rel)) {
@@ -548,7 +552,7 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
                 }
                 return 0;
             }
-            r.busy.store(0, std::memory_order_release);
+            r.busy.fetch_sub(1, std::memory_order_release);
             L.valid = false;
         }
         // New lease on the open slot: LM indices and room for LM packets of

@@ -94,6 +94,20 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
 // Batch kernel launch, bucketing a large ragged batch by length first.
 int launch_ordered(int alg, KArgs a, hipStream_t s);
 
+// The two batch paths of lcb_hash_batch (lcb_hash_gpu.cpp), on the current
+// device.  batch_device enqueues on `s`; batch_host stages through `stage`
+// (nullptr: the calling thread's own staging context).  `init`: CRC
+// X_update() values (nullptr otherwise).
+struct Stage;
+int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
+                 const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init);
+int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
+               const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
+               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage);
+Stage* stage_acquire(int dev);      // pooled staging context (multi-device workers)
+void stage_release(Stage* st);
+
 // Host-memory helpers shared by the host-mode pipelines.
 bool is_pinned(const void* p);  // page-locked (DMA-able) host memory
 struct Piece {

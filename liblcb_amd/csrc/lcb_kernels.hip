@@ -26,7 +26,7 @@ __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint
 template <class H>
 __device__ __forceinline__ void md_body(H& st, const KArgs& a, const uint8_t* msg, uint64_t len,
                                         uint64_t prefix) {
-    if (LCB_UNIFORM_PAD && !a.lengths && a.fixed_len % H::kBlock == 0) {
+    if (!a.lengths && a.fixed_len % H::kBlock == 0) {
         md_full_blocks(st, msg, (uint64_t)a.fixed_len / H::kBlock);
         md_pad_only(st, (uint64_t)a.fixed_len + prefix);
     } else {
@@ -62,32 +62,15 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 // workload and any array of equal-size records): each wave streams line L+1
 // of its 64 records into LDS (LdsLineStream, hash_device.hpp) while the two
 // 64-B blocks of line L are compressed.  Bytes after the last whole line go
-// through the generic loader.
-// LCB_LDS_DEPTH lines in flight per wave (8 KiB of LDS each), LCB_FIXED_WPG
-// waves per workgroup.
-#ifndef LCB_LDS_DEPTH
-#define LCB_LDS_DEPTH 1
-#endif
-#ifndef LCB_FIXED_WPG
-#define LCB_FIXED_WPG 4
-#endif
-#ifndef LCB_DMA_PRIO
-#define LCB_DMA_PRIO 0
-#endif
-// LCB_FIXED_OCC: pass the algorithm's occupancy target (capped at the 5
-// waves per SIMD the LDS allows) as the kernel's waves-per-SIMD bound.
-#ifndef LCB_FIXED_OCC
-#define LCB_FIXED_OCC 0
-#endif
-template <class H>
-constexpr int fixed_occ() { return LCB_FIXED_OCC ? (H::kOcc < 5 ? H::kOcc : 5) : 1; }
+// through the generic loader.  One line in flight per wave (8 KiB of LDS),
+// 4 waves per workgroup, 5 workgroups per CU (the whole 160 KiB); deeper
+// per-wave buffering and half-line stages measured slower
+// (profiles/r1_lds_depth_ab.txt, profiles/r1_lds_half_ab.txt).
 template <class H, bool kHmac>
-__global__ __launch_bounds__(64 * LCB_FIXED_WPG, fixed_occ<H>()) void md_fixed_lds_kernel(KArgs a) {
-    constexpr int kDepth = LCB_LDS_DEPTH, kWpg = LCB_FIXED_WPG;
-    static_assert(kDepth >= 1 && kDepth <= 3, "1..3 lines in flight");
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kWpg][kDepth * 8192];
+__global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * kWpg + wv) * 64;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
     const uint64_t last = a.count - 1;
     const uint64_t nlines = a.fixed_len / 128;
@@ -101,38 +84,15 @@ __global__ __launch_bounds__(64 * LCB_FIXED_WPG, fixed_occ<H>()) void md_fixed_l
     } else {
         st.init();
     }
-#ifndef LCB_EXP_SPLIT  // time-split experiments: 1 = no loads, 2 = no compression
-#define LCB_EXP_SPLIT 0
-#endif
-    if (LCB_EXP_SPLIT != 1) {
-#pragma unroll
-        for (int d = 0; d < kDepth; ++d)
-            if ((uint64_t)d < nlines) ls.issue(d, d);
-    }
+    if (nlines) ls.issue(0);
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
-        if (LCB_EXP_SPLIT == 1) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) w[k] = lane * 0x9e3779b9u + (uint32_t)L * 977u + k;
-        } else {
-            const uint32_t buf = (uint32_t)(L % kDepth);
-            const uint64_t later = nlines - 1 - L;  // lines issued after L (capped by depth)
-            if (LCB_DMA_PRIO) __builtin_amdgcn_s_setprio(3);  // take + re-issue ahead of other waves' VALU
-            if (kDepth >= 3 && later >= 2) ls.take<2>(w, w + 16, buf);
-            else if (kDepth >= 2 && later >= 1) ls.take<1>(w, w + 16, buf);
-            else ls.take<0>(w, w + 16, buf);  // line L -> VGPRs, its buffer free again
-            if (L + kDepth < nlines) ls.issue(L + kDepth, buf);
-            if (LCB_DMA_PRIO) __builtin_amdgcn_s_setprio(0);
-        }
-        if (LCB_EXP_SPLIT == 2) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) st.s[k % (sizeof(st.s) / sizeof(st.s[0]))] ^= w[k];
-            continue;
-        }
+        ls.take(w, w + 16);                 // line L -> VGPRs, its buffer free again
+        if (L + 1 < nlines) ls.issue(L + 1);
         if constexpr (H::kBlock == 128) {
-            st.compress(w);              // one SHA-384/512 block per line
+            st.compress(w);                 // one SHA-384/512 block per line
         } else {
-            st.compress(w);              // two 64-B blocks per line
+            st.compress(w);                 // two 64-B blocks per line
             st.compress(w + 16);
         }
     }
@@ -140,148 +100,10 @@ __global__ __launch_bounds__(64 * LCB_FIXED_WPG, fixed_occ<H>()) void md_fixed_l
     if (i > last) return;
     const uint8_t* msg = a.data + i * a.stride + nlines * 128;
     const uint64_t tail = (uint64_t)a.fixed_len - nlines * 128;
-    if (LCB_UNIFORM_PAD && tail == 0)  // wave-uniform: schedule of the pad block on the SALU
+    if (tail == 0)  // wave-uniform: schedule of the pad block on the SALU
         md_pad_only(st, prefix + nlines * 128);
     else
         md_message(st, msg, tail, prefix + nlines * 128);
-    uint32_t dw[H::kDigest / 4];
-    st.digest_words(dw);
-    if (kHmac) {
-        H o;
-        load_words(o.s, a.mid + kMidWords);
-        md_outer(o, dw);
-        o.digest_words(dw);
-    }
-    store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
-}
-
-// ------------------------------------------- MD family, ragged LDS-DMA path
-// Ragged batches (offsets and/or lengths, normally bucketed by length so a
-// wave's records have similar block counts): the whole 128-B lines of the
-// wave's 64 records stream through LDS like the fixed-stride path
-// (GatherLineStream), each lane compressing only its own lines; the tail and
-// padding go through the per-lane loader.  A wave whose records do not all
-// start 16-B aligned takes the per-lane path for the whole message.
-// Parity-green but off: on the C4 mix ({64 B, 1 KiB, 64 KiB}) it is 11 %
-// slower for MD5 and within 1 % for SHA-1/SHA-256 (profiles/r1_gather_ab.txt).
-// The 5.3K waves of 64 KiB records outnumber the 5 x 4 LDS-limited wave
-// slots per CU (5,120 chip-wide), so the last ones run alone, where the
-// per-lane kernel (8 waves per SIMD) holds all of them at once.
-#ifndef LCB_GATHER_LDS
-#define LCB_GATHER_LDS 0
-#endif
-template <class H, bool kHmac>
-__global__ __launch_bounds__(256) void md_gather_lds_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
-    if (wave_first >= a.count) return;  // wave-uniform
-    const uint64_t last = a.count - 1, i = wave_first + lane, ic = i > last ? last : i;
-    const uint64_t idx = a.order ? (uint64_t)gptr(a.order)[ic] : ic;
-    const uint8_t* msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
-    const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
-    H st;
-    uint64_t prefix = 0;
-    if (kHmac) {
-        load_words(st.s, a.mid);
-        prefix = H::kBlock;
-    } else {
-        st.init();
-    }
-    const uint32_t nl = (uint32_t)((len >> 7) < 0xffffffu ? (len >> 7) : 0xffffffu);  // lines streamed
-    const bool ok = nl == 0 || (reinterpret_cast<uintptr_t>(msg) & 15u) == 0;
-    uint64_t done = 0;
-    if (__all(ok)) {  // wave-uniform
-        uint32_t mx = nl;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const uint32_t v = (uint32_t)__shfl_xor((int)mx, o, 64);
-            mx = v > mx ? v : mx;
-        }
-        if (mx > 0) {
-            const int lead = (int)__builtin_ctzll(__ballot(nl == mx));  // a lane with mx lines
-            const uint64_t lead_msg =
-                __shfl((unsigned long long)reinterpret_cast<uintptr_t>(msg), lead, 64);
-            const uint8_t* base = nl ? msg : reinterpret_cast<const uint8_t*>(lead_msg);
-            GatherLineStream gs;
-            gs.init_gather(base, (nl ? nl : mx) - 1, lane, &slab[wv][0]);
-            gs.issue_clamped(0);
-            for (uint32_t L = 0; L < mx; ++L) {
-                uint32_t w[32];
-                gs.take(w, w + 16);
-                if (L + 1 < mx) gs.issue_clamped(L + 1);
-                if (L < nl) {
-                    if constexpr (H::kBlock == 128) {
-                        st.compress(w);
-                    } else {
-                        st.compress(w);
-                        st.compress(w + 16);
-                    }
-                }
-            }
-            done = (uint64_t)nl * 128;
-        }
-    }
-    if (i > last) return;
-    md_message(st, msg + done, len - done, prefix + done);
-    uint32_t dw[H::kDigest / 4];
-    st.digest_words(dw);
-    if (kHmac) {
-        H o;
-        load_words(o.s, a.mid + kMidWords);
-        md_outer(o, dw);
-        o.digest_words(dw);
-    }
-    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
-}
-
-// Half-line stages (LdsHalfStream): one 64-B block of each record per stage,
-// LCB_HALF_DEPTH stages in flight per wave; 64-B-block algorithms only.
-#ifndef LCB_HALF_DEPTH
-#define LCB_HALF_DEPTH 2
-#endif
-template <class H, bool kHmac>
-__global__ __launch_bounds__(64 * LCB_FIXED_WPG) void md_fixed_half_kernel(KArgs a) {
-    static_assert(H::kBlock == 64, "64-B blocks");
-    constexpr int kDepth = LCB_HALF_DEPTH, kWpg = LCB_FIXED_WPG;
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kWpg][kDepth * 4096];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * kWpg + wv) * 64;
-    if (wave_first >= a.count) return;  // wave-uniform
-    const uint64_t last = a.count - 1;
-    const uint64_t nblk = a.fixed_len / 64;
-    LdsHalfStream ls;
-    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
-    H st;
-    uint64_t prefix = 0;
-    if (kHmac) {
-        load_words(st.s, a.mid);
-        prefix = H::kBlock;
-    } else {
-        st.init();
-    }
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d)
-        if ((uint64_t)d < nblk) ls.issue(d, d);
-    for (uint64_t B = 0; B < nblk; ++B) {
-        uint32_t w[16];
-        const uint32_t buf = (uint32_t)(B % kDepth);
-        const uint64_t later = nblk - 1 - B;
-        if (kDepth >= 4 && later >= 3) ls.take<3>(w, buf);
-        else if (kDepth >= 3 && later >= 2) ls.take<2>(w, buf);
-        else if (kDepth >= 2 && later >= 1) ls.take<1>(w, buf);
-        else ls.take<0>(w, buf);
-        if (B + kDepth < nblk) ls.issue(B + kDepth, buf);
-        st.compress(w);
-    }
-    const uint64_t i = wave_first + lane;
-    if (i > last) return;
-    const uint8_t* msg = a.data + i * a.stride + nblk * 64;
-    const uint64_t tail = (uint64_t)a.fixed_len - nblk * 64;
-    if (LCB_UNIFORM_PAD && tail == 0)
-        md_pad_only(st, prefix + nblk * 64);
-    else
-        md_message(st, msg, tail, prefix + nblk * 64);
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kHmac) {
@@ -326,18 +148,14 @@ __global__ void md_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t k
 }
 
 // ------------------------------------------------------------------ GOST
+// Two waves per SIMD: the 64 KiB rotated LPS image (gost_device.hpp GostRot)
+// leaves room for two 256-thread workgroups per CU.
 template <bool k256, bool kHmac>
-__global__ __launch_bounds__(256, LCB_OCC_GOST) void gost_batch_kernel(KArgs a) {
-#if LCB_GOST_ROT
+__global__ __launch_bounds__(256, 2) void gost_batch_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
     gost_stage_rot(Timg);
     GostRot T;
     T.init((lds_u8*)Timg);
-#else
-    __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
-    gost_stage_table(Timg);
-    const GostFlat T{Timg};
-#endif
     uint64_t idx, len;
     const uint8_t* msg;
     if (!msg_at(a, idx, msg, len)) return;
@@ -508,30 +326,15 @@ void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, u
 // ------------------------------------------------------------- launchers
 static inline dim3 grid_for(uint64_t count) { return dim3((unsigned)((count + 255) / 256)); }
 
-// The LDS-DMA fast path applies to fixed-stride, 16-B aligned records of at
-// least one whole 128-B line, for the HBM-bound 64-B-block algorithms.
-static bool fixed_lds_ok(const KArgs& a) { return LCB_FIXED_LDS && fixed_stride_lines(a); }
-
 template <class H>
 static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
     if constexpr (H::kLdsStream) {
-        if (fixed_lds_ok(a)) {
-            const dim3 grid((unsigned)((a.count + 64 * LCB_FIXED_WPG - 1) / (64 * LCB_FIXED_WPG)));
-            const dim3 block(64 * LCB_FIXED_WPG);
-            if constexpr (H::kBlock == 64 && H::kHalfStream) {
-                if (hmac) hipLaunchKernelGGL((md_fixed_half_kernel<H, true>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((md_fixed_half_kernel<H, false>), grid, block, 0, s, a);
-                return;
-            }
-            if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid, block, 0, s, a);
-            return;
-        }
-    }
-    if constexpr (H::kLdsStream) {
-        if (LCB_GATHER_LDS && a.order) {  // bucketed ragged batch
-            if (hmac) hipLaunchKernelGGL((md_gather_lds_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((md_gather_lds_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
+        // LDS-DMA fast path: fixed-stride, 16-B aligned records of at least one
+        // whole 128-B line.
+        if (fixed_stride_lines(a)) {
+            const dim3 grid((unsigned)((a.count + 255) / 256));
+            if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid, dim3(256), 0, s, a);
             return;
         }
     }

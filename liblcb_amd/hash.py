@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (ALG_IDS, DIGEST_SIZE, F_DEVICE, GOST256, GOST512, MD5, SHA1, SHA224,
+from ._lib import (ALG_IDS, DIGEST_SIZE, F_COPY_PARTS, F_DEVICE, GOST256, GOST512, MD5, SHA1, SHA224,
                    SHA256, SHA384, SHA512, check, lib)
 
 __all__ = [
@@ -27,6 +27,7 @@ __all__ = [
     "sha1_get_digest_batch", "sha1_hmac_get_digest_batch", "sha2_get_digest_batch",
     "sha2_hmac_get_digest_batch", "gost3411_2012_get_digest_batch",
     "gost3411_2012_hmac_get_digest_batch", "gen_synthetic", "sha2_alg", "gost_alg",
+    "partition", "hash_batch_multi",
 ]
 
 
@@ -60,6 +61,34 @@ def _layout(count, offsets, lengths, stride, fixed_len, nbytes):
     return int(count), int(stride or 0), int(fixed_len or 0)
 
 
+def _check_extent(nbytes, count, offsets, lengths, stride, fixed_len):
+    """Every described message must lie inside the `nbytes` of `data`: the
+    C-ABI trusts the description (out-of-range host reads would leak or
+    crash; out-of-range device reads fault the GPU).  Works on numpy arrays
+    and on device tensors (one reduction, one synchronisation)."""
+    if count == 0:
+        return
+    for name, t in (("offsets", offsets), ("lengths", lengths)):
+        if t is not None and int(t.shape[0]) < count:
+            raise ValueError("%s has %d entries, count is %d" % (name, int(t.shape[0]), count))
+    if offsets is None and lengths is None:
+        end = (count - 1) * stride + fixed_len
+    elif isinstance(offsets if offsets is not None else lengths, torch.Tensor):
+        o = offsets[:count].to(torch.int64) if offsets is not None else \
+            torch.arange(count, dtype=torch.int64, device=lengths.device) * stride
+        n = lengths[:count].to(torch.int64) & 0xFFFFFFFF if lengths is not None else fixed_len
+        end = int((o + n).max().item())
+        if int(o.min().item()) < 0:
+            raise ValueError("negative offset")
+    else:
+        o = offsets[:count].astype(np.uint64) if offsets is not None else \
+            np.arange(count, dtype=np.uint64) * np.uint64(stride)
+        n = lengths[:count].astype(np.uint64) if lengths is not None else np.uint64(fixed_len)
+        end = int((o + n).max())
+    if end > nbytes:
+        raise ValueError("messages extend to byte %d of a %d-byte buffer" % (end, nbytes))
+
+
 def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None,
                fixed_len=None, key=None, out=None):
     """Digest (or HMAC when `key` is given) of every message of a batch.
@@ -84,8 +113,10 @@ def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None
         for t, dt in ((offsets, (torch.int64, torch.uint64)), (lengths, (torch.int32, torch.uint32))):
             if t is not None:
                 assert _is_dev(t) and t.dtype in dt and t.is_contiguous() and t.device == data.device
+        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
         if out is None:
             out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+        assert out.numel() >= count * D
         with torch.cuda.device(data.device):
             stream = torch.cuda.current_stream(data.device).cuda_stream
             check(L.lcb_hash_batch(alg, kptr, klen, data.data_ptr(),
@@ -97,6 +128,7 @@ def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None
     if isinstance(data, (bytes, bytearray, memoryview)):
         data = np.frombuffer(bytes(data), dtype=np.uint8)
     data = np.ascontiguousarray(data, dtype=np.uint8)
+    nbytes = data.size
     if data.size == 0:
         data = np.zeros(1, dtype=np.uint8)
     if offsets is not None:
@@ -104,8 +136,10 @@ def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None
     if lengths is not None:
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
     count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
     if out is None:
         out = np.empty((count, D), dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= count * D
     check(L.lcb_hash_batch(alg, kptr, klen, data.ctypes.data,
                            offsets.ctypes.data if offsets is not None else None,
                            lengths.ctypes.data if lengths is not None else None,
@@ -170,3 +204,62 @@ def gen_synthetic(seed, nbytes, start=0, device="cuda", out=None):
         stream = torch.cuda.current_stream(out.device).cuda_stream
         check(lib().lcb_hash_gen_synthetic(seed, start, out.data_ptr(), int(nbytes), stream))
     return out[:int(nbytes)]
+
+
+def partition(nparts, *, lengths=None, count=None, fixed_len=0):
+    """lcb_hash_partition: contiguous message ranges of balanced work
+    (bytes + one 64-B padding block per message) -> uint64 array `first` of
+    nparts + 1 entries; part p = messages [first[p], first[p+1])."""
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        count = int(lengths.size) if count is None else int(count)
+        assert lengths.size >= count
+    first = np.zeros(int(nparts) + 1, np.uint64)
+    check(lib().lcb_hash_partition(lengths.ctypes.data if lengths is not None else None, int(count),
+                                   int(fixed_len), int(nparts), first.ctypes.data))
+    return first
+
+
+def hash_batch_multi(devs, alg, data, *, offsets=None, lengths=None, count=None, stride=None,
+                     fixed_len=None, key=None, out=None, copy_parts=False):
+    """lcb_hash_batch_multi: the batch split by `partition` over the HIP
+    devices `devs` (repeats allowed) and hashed on all of them at once.
+    Device tensors must live on devs[0]; numpy input runs in host mode."""
+    if isinstance(alg, str):
+        alg = ALG_IDS[alg]
+    D = DIGEST_SIZE[alg]
+    kb = None if key is None else bytes(key)
+    kptr = ctypes.c_char_p(kb) if kb is not None else None
+    klen = len(kb) if kb is not None else 0
+    dv = (ctypes.c_int * len(devs))(*devs)
+    if _is_dev(data):
+        assert data.dtype == torch.uint8 and data.is_contiguous() and data.device.index == devs[0]
+        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
+        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
+        if out is None:
+            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+        torch.cuda.synchronize(data.device)     # inputs written on torch's stream are complete
+        check(lib().lcb_hash_batch_multi(dv, len(devs), alg, kptr, klen, data.data_ptr(),
+                                         offsets.data_ptr() if offsets is not None else None,
+                                         lengths.data_ptr() if lengths is not None else None,
+                                         count, stride, fixed_len, out.data_ptr(),
+                                         F_DEVICE | (F_COPY_PARTS if copy_parts else 0)))
+        return out
+    data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8)
+                                if isinstance(data, (bytes, bytearray, memoryview)) else data, dtype=np.uint8)
+    nbytes = data.size
+    if data.size == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
+    if out is None:
+        out = np.empty((count, D), dtype=np.uint8)
+    check(lib().lcb_hash_batch_multi(dv, len(devs), alg, kptr, klen, data.ctypes.data,
+                                     offsets.ctypes.data if offsets is not None else None,
+                                     lengths.ctypes.data if lengths is not None else None,
+                                     count, stride, fixed_len, out.ctypes.data, 0))
+    return out

@@ -23,6 +23,16 @@ def mixed_lengths(seed, count):
     return out
 
 
+def mixed_lengths_np(seed, count):
+    """mixed_lengths, vectorised (uint32 array, same values)."""
+    with np.errstate(over="ignore"):
+        z = np.arange(count, dtype=np.uint64) + np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return np.array([64, 1024, 65536], np.uint32)[(z % np.uint64(3)).astype(np.int64)]
+
+
 def layout(entry):
     """-> dict(seed, nbytes, offsets|None, lengths|None, count, stride, fixed_len, key)."""
     name = entry["name"]

@@ -292,3 +292,47 @@ def test_host_mode_pinned_direct_dma(gpu, batches):
         d = gpu.hash_batch(ALG[e["alg"]], pinned.numpy(), offsets=L["offsets"], lengths=L["lengths"],
                            count=L["count"], stride=L["stride"], fixed_len=L["fixed_len"], key=L["key"])
         check_entry(e, d)
+
+
+@pytest.fixture(scope="module")
+def large():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "large.json")))
+
+
+def test_c5_full_size_one_gpu(gpu, large):
+    """BASELINE config C5 (8M x 1 KiB = 8 GiB) on ONE MI355X, every
+    algorithm: the whole digest array and each of the 8 per-GPU shards of
+    the weak-scaling bench against the reference's digest-of-digests
+    (tests/golden/large.json)."""
+    import hashlib
+    fx = large["C5_8M_x_1k"]
+    n, sh = fx["count"], fx["shard"]
+    data = gpu.gen_synthetic(large["seed"], n * 1024)
+    for name, alg in ALG.items():
+        d = gpu.hash_batch(alg, data, count=n, stride=1024, fixed_len=1024).cpu().numpy()
+        assert dod(d) == fx["algs"][name]["dod"], name
+        shards = [hashlib.sha256(d[k * sh:(k + 1) * sh].tobytes()).hexdigest() for k in range(n // sh)]
+        assert shards == fx["algs"][name]["shard_dod"], name
+    del data
+    torch.cuda.empty_cache()
+
+
+def test_c4_full_size(gpu, large):
+    """BASELINE config C4 (1M buffers of {64 B, 1 KiB, 64 KiB}, 21.7 GiB
+    packed, the bench's ragged_c4 workload), every algorithm, against the
+    reference's digest-of-digests."""
+    from tests.golden_util import mixed_lengths_np
+    fx = large["C4_1M_mixed"]
+    lens = mixed_lengths_np(large["seed"], fx["count"])
+    offs = np.zeros(lens.size, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    assert int(lens.sum()) == fx["total_bytes"]
+    data = gpu.gen_synthetic(large["seed"], fx["total_bytes"])
+    dl, do = dev(lens, np.int32), dev(offs, np.int64)
+    for name, alg in ALG.items():
+        d = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        assert dod(d) == fx["algs"][name]["dod"], name
+    del data
+    torch.cuda.empty_cache()

@@ -1,0 +1,126 @@
+"""Multi-device batches (include/lcb_hash_gpu.h: lcb_hash_partition,
+lcb_hash_batch_multi).
+
+CPU: the work-balanced split (bytes + one padding block per message) on the
+C4 length mix keeps every part within 1 % of the mean; fixed lengths split
+into equal counts; degenerate shapes.  GPU (one MI355X on the box): the
+multi-device call with devs = {0} equals lcb_hash_batch; devs = {0, 0, 0}
+runs three concurrent parts on one device (host mode: three staging
+pipelines; device mode: in place, and through the peer-copy scatter/gather
+path forced by LCB_HASH_F_COPY_PARTS), all checked against the oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle.pyoracle import gen_stream
+from tests.golden_util import SEED, mixed_lengths_np
+
+
+def _lcb():
+    import liblcb_amd
+    try:
+        liblcb_amd.lib()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    return liblcb_amd
+
+
+@pytest.mark.parametrize("nparts", [2, 4, 8])
+def test_partition_balances_c4_bytes(nparts):
+    lcb = _lcb()
+    lens = mixed_lengths_np(SEED, 1 << 20)
+    first = lcb.partition(nparts, lengths=lens)
+    assert first[0] == 0 and first[-1] == lens.size and np.all(np.diff(first.astype(np.int64)) >= 0)
+    cum = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)])
+    part_bytes = cum[first[1:].astype(np.int64)] - cum[first[:-1].astype(np.int64)]
+    mean = cum[-1] / nparts
+    assert part_bytes.max() <= 1.01 * mean, (part_bytes, mean)
+    # the rule: first[p] is where the work prefix (bytes + 64 per message) crosses p/N
+    w = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 64)])
+    for p in range(1, nparts):
+        i = int(first[p])
+        t = w[-1] * p // nparts
+        assert w[i] - (int(lens[i - 1]) + 64) // 2 < t <= w[i] + (int(lens[i]) + 64) // 2
+
+
+def test_partition_fixed_and_degenerate():
+    lcb = _lcb()
+    assert lcb.partition(8, count=8 << 20, fixed_len=1024).tolist() == [k << 20 for k in range(9)]
+    assert lcb.partition(3, count=10, fixed_len=5).tolist() == [0, 3, 6, 10]
+    assert lcb.partition(4, count=2, fixed_len=5).tolist() == [0, 0, 1, 1, 2]
+    assert lcb.partition(1, lengths=np.array([5, 6], np.uint32)).tolist() == [0, 2]
+    z = lcb.partition(2, lengths=np.zeros(10, np.uint32))      # empty messages still cost a block
+    assert z.tolist() == [0, 5, 10]
+    assert lcb.partition(3, lengths=np.zeros(0, np.uint32)).tolist() == [0, 0, 0, 0]
+    import errno
+    with pytest.raises(lcb.LcbHashError) as e:
+        lcb.partition(0, count=4)
+    assert e.value.errno == errno.EINVAL
+
+
+def _ragged(seed, n):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    lens[rng.integers(0, n, 20)] = 65536
+    offs = np.zeros(n, np.uint64)
+    pos = 3
+    for i in range(n):
+        offs[i] = pos
+        pos += int(lens[i]) + int(rng.integers(0, 5))
+    return gen_stream(seed, pos), offs, lens
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", [[0], [0, 0, 0]])
+def test_multi_host_mode(gpu, oracle, devs):
+    data, offs, lens = _ragged(5, 9000)
+    for alg, key in ((1, None), (4, b"radius"), (7, None)):
+        got = gpu.hash_batch_multi(devs, alg, data, offsets=offs, lengths=lens, key=key)
+        assert np.array_equal(got, oracle.batch(alg, data, offs, lens, key=key)), (alg, devs)
+    fx = gen_stream(6, 5000 * 1024)
+    got = gpu.hash_batch_multi(devs, 2, fx, count=5000, stride=1024, fixed_len=1000)
+    assert np.array_equal(got, oracle.batch(2, fx, count=5000, stride=1024, fixed_len=1000))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs,copy", [([0], False), ([0, 0, 0], False), ([0, 0, 0], True), ([0, 0], True)])
+def test_multi_device_mode(gpu, oracle, devs, copy):
+    import torch
+    data, offs, lens = _ragged(8, 9000)
+    dd = torch.as_tensor(data, device="cuda:0")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda:0")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda:0")
+    for alg, key in ((1, None), (6, b"k" * 200), (8, None)):
+        got = gpu.hash_batch_multi(devs, alg, dd, offsets=do, lengths=dl, key=key, copy_parts=copy)
+        assert np.array_equal(got.cpu().numpy(), oracle.batch(alg, data, offs, lens, key=key)), (alg, devs)
+    # lengths without offsets (message i at i * stride) and plain fixed stride
+    n = 4000
+    fx = gen_stream(9, n * 512)
+    fl = (np.arange(n) % 513).astype(np.uint32)
+    got = gpu.hash_batch_multi(devs, 4, torch.as_tensor(fx, device="cuda:0"), stride=512,
+                               lengths=torch.as_tensor(fl.astype(np.int32), device="cuda:0"), copy_parts=copy)
+    exp = oracle.batch(4, fx, None, fl, count=n, stride=512)
+    assert np.array_equal(got.cpu().numpy(), exp)
+    got = gpu.hash_batch_multi(devs, 1, torch.as_tensor(fx, device="cuda:0"), count=n, stride=512,
+                               fixed_len=512, copy_parts=copy)
+    assert np.array_equal(got.cpu().numpy(), oracle.batch(1, fx, count=n, stride=512, fixed_len=512))
+
+
+@pytest.mark.gpu
+def test_multi_single_device_equals_batch(gpu):
+    """devs = {0}: the same digests as lcb_hash_batch on the bench workload."""
+    n = 1 << 18
+    data = gpu.gen_synthetic(SEED, n * 1024)
+    a = gpu.hash_batch(1, data, count=n, stride=1024, fixed_len=1024)
+    b = gpu.hash_batch_multi([0], 1, data, count=n, stride=1024, fixed_len=1024)
+    assert bool((a == b).all())
+
+
+@pytest.mark.gpu
+def test_multi_errors(gpu):
+    import errno
+    import torch
+    d = torch.zeros(1024, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(gpu.LcbHashError) as e:
+        gpu.hash_batch_multi([0, 99], 1, d, count=1, fixed_len=16)
+    assert e.value.errno == errno.ENODEV

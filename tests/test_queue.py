@@ -206,3 +206,32 @@ def test_native_producers(gpu, oracle, tmp_path, alg, key):
     want = oracle.batch_fixed_mt(alg, gen_stream(SEED, n * size), n, size, size,
                                  key=bytes.fromhex(key) if key else None)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_stale_lease_across_generations(gpu, oracle):
+    """One producer goes idle holding a lease while the others cycle the slots
+    through many generations (2 slots, 16-message batches); when it wakes its
+    stale lease must neither be written nor disturb the busy count of the
+    record's current owner (lease records are reused every generation)."""
+    from liblcb_amd.queue import HashQueue
+    pkts = _packets(23, 6000, 0, 400)
+    want = _oracle_digests(oracle, MD5, pkts)
+    got = np.zeros((len(pkts), 16), np.uint8)
+    with HashQueue(MD5, max_batch_msgs=64, batches=2, align=1) as q:
+        def sleeper():
+            for i in range(0, 600, 3):
+                q.submit(pkts[i], out=got[i])
+                time.sleep(0.002)     # idle while the others reopen the slots
+        def busy(t):
+            for i in range(600 + t, len(pkts), 2):
+                q.submit(pkts[i], out=got[i])
+            for i in range(1 + t, 600, 3):
+                q.submit(pkts[i], out=got[i])
+        th = [threading.Thread(target=sleeper)] + [threading.Thread(target=busy, args=(t,)) for t in range(2)]
+        [x.start() for x in th]
+        [x.join() for x in th]
+        q.wait()
+        st = q.stats()
+    assert np.array_equal(got, want)
+    assert st["packets"] == len(pkts) and st["batches"] > 50
