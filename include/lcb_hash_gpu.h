@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define LCB_HASH_GPU_ABI_VERSION	2
+#define LCB_HASH_GPU_ABI_VERSION	3
 
 /* Algorithm ids. */
 #define LCB_HASH_MD5		1	/* md5.h */
@@ -82,6 +82,36 @@ int	lcb_hash_batch(int alg, const uint8_t *key, size_t key_len,
 	    const uint8_t *data, const uint64_t *offsets, const uint32_t *lengths,
 	    size_t count, uint64_t stride, uint32_t fixed_len,
 	    uint8_t *digests, uint32_t flags, void *stream);
+
+/*
+ * Keyed batches: message i uses key k = key_index[i] (NULL: key 0) of a key
+ * table — the RADIUS shapes, one shared secret per peer
+ * (src/proto/radius_client.c:242,886,1025):
+ *   LCB_HASH_KEY_HMAC    digest_i = HMAC(K_k, m_i)   RFC 2104 as the
+ *                        *_hmac_get_digest functions; Message-Authenticator
+ *                        (include/proto/radius.h:850-919)
+ *   LCB_HASH_KEY_PREFIX  digest_i = H(K_k || m_i)    User-Password hiding
+ *                        (radius.h:745-830: MD5(secret || authenticator)
+ *                        and MD5(secret || c_j) from a copied key context)
+ *   LCB_HASH_KEY_SUFFIX  digest_i = H(m_i || K_k)    packet authenticator
+ *                        (radius.h:1315-1377: MD5(packet || secret))
+ * Key k = keys + (key_offsets ? key_offsets[k] : 0), key_lengths[k] bytes;
+ * keys, key_offsets and key_lengths are HOST memory.  key_index lives where
+ * the batch does (device memory with LCB_HASH_F_DEVICE).  Per-key state
+ * (HMAC ipad/opad mid-states, the prefix's whole-block state) is computed
+ * once per key on the device.  Host mode: an index >= nkeys is EINVAL;
+ * device mode: it selects the last key.  The call waits for the key table
+ * upload (the host arrays may be released on return); with
+ * LCB_HASH_F_DEVICE the batch itself stays asynchronous on `stream`.
+ */
+#define LCB_HASH_KEY_HMAC	1
+#define LCB_HASH_KEY_PREFIX	2
+#define LCB_HASH_KEY_SUFFIX	3
+int	lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t *keys,
+	    const uint64_t *key_offsets, const uint32_t *key_lengths, size_t nkeys,
+	    const uint32_t *key_index, const uint8_t *data, const uint64_t *offsets,
+	    const uint32_t *lengths, size_t count, uint64_t stride,
+	    uint32_t fixed_len, uint8_t *digests, uint32_t flags, void *stream);
 
 /* Reference-named batch entry points. ---------------------------------- */
 

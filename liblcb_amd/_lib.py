@@ -27,6 +27,7 @@ DIGEST_SIZE = {MD5: 16, SHA1: 20, SHA224: 28, SHA256: 32, SHA384: 48, SHA512: 64
 BLOCK_SIZE = {a: (128 if a in (SHA384, SHA512) else 64) for a in DIGEST_SIZE}
 F_DEVICE = 0x1
 F_COPY_PARTS = 0x100
+KEY_HMAC, KEY_PREFIX, KEY_SUFFIX = 1, 2, 3
 
 _lib = None
 
@@ -57,6 +58,8 @@ SIGNATURES = [
      [c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
     ("gost3411_2012_hmac_get_digest_batch", ctypes.c_int,
      [c_sz, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp, c_u32, c_vp]),
+    ("lcb_hash_batch_keyed", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp, c_sz, c_vp] + _PLAIN),
     ("lcb_hash_partition", ctypes.c_int, [c_vp, c_sz, c_u32, c_sz, c_vp]),
     ("lcb_hash_batch_multi", ctypes.c_int,
      [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32]),

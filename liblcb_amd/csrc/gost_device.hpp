@@ -336,4 +336,30 @@ __device__ __forceinline__ void gost_message(Gost<k256>& st, const uint8_t* msg,
     st.finish(w, rem, T);
 }
 
+// Virtual message A[0, la) || B[0, lb) (keyed batches): as gost_message,
+// the seam block assembled from both.
+template <bool k256, class Tab>
+__device__ __forceinline__ void gost_message2(Gost<k256>& st, const uint8_t* A, uint64_t la, const uint8_t* B,
+                                              uint64_t lb, const Tab& T) {
+    uint32_t w[16];
+    const uint64_t nA = la / 64;
+    for (uint64_t b = 0; b < nA; ++b) {
+        load_full64(A + 64 * b, w);
+        st.block(w, 512, T);
+    }
+    uint64_t done = nA * 64;
+    const uint64_t total = la + lb;
+    while (done < la && done + 64 <= total) {
+        load_vblock64(A, la, B, lb, done, w);
+        st.block(w, 512, T);
+        done += 64;
+    }
+    if (done >= la) {
+        gost_message(st, B + (done - la), total - done, T);
+        return;
+    }
+    load_vblock64(A, la, B, lb, done, w);
+    st.finish(w, (uint32_t)(total - done), T);
+}
+
 }  // namespace lcbgpu

@@ -170,6 +170,49 @@ __device__ __forceinline__ void load_tail64(const uint8_t* p, uint32_t rem, uint
     }
 }
 
+// OR the bytes p[lo .. hi) (0 <= lo <= hi <= 64) into raw LE byte positions
+// lo .. hi of w.  `p` itself may lie outside the caller's buffer: only the
+// aligned dwords holding at least one byte of [p + lo, p + hi) are loaded.
+__device__ __forceinline__ void or_window64(const uint8_t* p, uint32_t lo, uint32_t hi, uint32_t w[16]) {
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(ip & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    // aligned dword k holds p bytes [4k - sh, 4k + 4 - sh)
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) d[k] = (4u * k < hi + sh && 4u * k + 4u > lo + sh) ? q[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        // bytes of word k inside [lo, hi)
+        const int b0 = (int)lo - 4 * k, b1 = (int)hi - 4 * k;
+        const uint32_t mlo = b0 <= 0 ? 0xffffffffu : (b0 >= 4 ? 0u : (0xffffffffu << (8 * b0)));
+        const uint32_t mhi = b1 >= 4 ? 0xffffffffu : (b1 <= 0 ? 0u : (0xffffffffu >> (32 - 8 * b1)));
+        w[k] |= v & mlo & mhi;
+    }
+}
+
+// Bytes [pos, pos + 64) of the virtual message V = A[0, la) || B[0, lb) as
+// raw LE words; bytes at or past la + lb are zero.  Keyed batches
+// (lcb_hash_batch_keyed) hash key || message and message || key this way
+// without a copy of either.
+__device__ __forceinline__ void load_vblock64(const uint8_t* A, uint64_t la, const uint8_t* B, uint64_t lb,
+                                              uint64_t pos, uint32_t w[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0u;
+    if (pos < la) {
+        const uint64_t n = la - pos;
+        or_window64(A + pos, 0, n < 64 ? (uint32_t)n : 64u, w);
+    }
+    const uint64_t end = la + lb;
+    if (pos + 64 > la && pos < end) {
+        const uint64_t b = pos > la ? pos : la;       // first V byte taken from B
+        const uint32_t s0 = (uint32_t)(b - pos);
+        const uint64_t e = pos + 64 < end ? pos + 64 : end;
+        or_window64(B + (b - la) - s0, s0, (uint32_t)(e - pos), w);
+    }
+}
+
 // OR byte value `b` into raw LE byte position `pos` (0..63) of w.
 __device__ __forceinline__ void put_byte(uint32_t w[16], uint32_t pos, uint32_t b) {
 #pragma unroll
@@ -189,6 +232,7 @@ struct Md5 {
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = false;  // no schedule to move: pad block via compress()
+    static constexpr int kTileOcc = 7;         // md_tiles_kernel: waves per SIMD (0: not used)
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -294,6 +338,7 @@ struct Sha1 {
     static constexpr bool kPairLoad = true;
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
+    static constexpr int kTileOcc = 0;   // the tile kernel spills at 80 VGPRs: ragged batches go per-lane
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -370,6 +415,7 @@ struct Sha256 {
     // Line stream on: 2.4 % faster than direct loads (profiles/r1_sha2_lds_ab.txt).
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
+    static constexpr int kTileOcc = 0;   // VALU-bound: ragged batches take the per-lane kernel
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132
@@ -466,6 +512,7 @@ struct Sha512 {
     // of 4; profiles/r1_sha2_lds_ab.txt, profiles/r1_fixed_occ_ab.txt).
     static constexpr bool kLdsStream = false;
     static constexpr bool kScalarPad = true;
+    static constexpr int kTileOcc = 0;   // VALU-bound: ragged batches take the per-lane kernel
     uint64_t s[8];
     __device__ __forceinline__ void init() {
         if (k384) {  // sha2.h:139-143
@@ -639,6 +686,12 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // Lanes beyond the last record load the last record (clamped) and must not
 // store.  The DMA stream carries the nt cache policy (every byte is read
 // once; kLdsAux).
+// Cache policy of the ragged (gather) line stream: default.  Records of a
+// packed ragged batch need not start on a 128-B line, so one streamed "line"
+// spans two cache lines; with nt the second is gone before the record's next
+// line asks for it (64 KiB records at a 64-B phase: 5.95 ms with nt, 4.70
+// default; profiles/r2_c4_tiles_ab.txt).
+constexpr int kGatherAux = 0;
 constexpr int kLdsAux = 2;  // cache policy of the LDS-DMA stream: nt (every byte is read once)
 struct LdsLineStream {
     const uint8_t* src[8];
@@ -670,10 +723,19 @@ struct LdsLineStream {
     // (raw LE words); the buffer is free again on return.
     __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16], uint32_t buf = 0) const {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t fj = (lane >> 1) & 7;
+        // LDS byte address of slot (k ^ fj): the row is 128-B aligned, so it
+        // is one v_xor of this lane's base with k << 4.  The base is hidden
+        // from the optimiser each call so the 8 addresses are re-formed here
+        // instead of being hoisted out of the caller's line loop (where they
+        // were spilled to scratch at 80 VGPRs).
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        using lds_cu4 = __attribute__((address_space(3))) const v4u;
+        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) + buf * 8192 +
+                     lane * 128 + ((lane >> 1) & 7) * 16;
+        asm volatile("" : "+v"(b));
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(slab + buf * 8192 + lane * 128 + ((k ^ fj) * 16));
+            const v4u v = *(lds_cu4*)(uintptr_t)(b ^ (uint32_t)(k << 4));
             uint32_t* d = (k < 4) ? (w0 + 4 * k) : (w1 + 4 * (k - 4));
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
@@ -686,7 +748,7 @@ struct LdsLineStream {
 // (the data is discarded; every DMA stays inside the record).  Bases and
 // limits are exchanged across lanes once, at init.
 struct GatherLineStream : LdsLineStream {
-    uint32_t lim[8];
+    uint32_t rem[8];   // advances left: lines of the record after the current one
     __device__ __forceinline__ void init_gather(const uint8_t* base, uint32_t last_line, uint32_t ln,
                                                 uint8_t* my_slab) {
         lane = ln;
@@ -695,18 +757,34 @@ struct GatherLineStream : LdsLineStream {
         for (int g = 0; g < 8; ++g) {
             const int j = 8 * g + (int)(ln >> 3);
             const uint64_t b = __shfl((unsigned long long)reinterpret_cast<uintptr_t>(base), j, 64);
-            lim[g] = (uint32_t)__shfl((int)last_line, j, 64);
+            rem[g] = (uint32_t)__shfl((int)last_line, j, 64);
             const uint32_t f = ((ln >> 4) + 4 * g) & 7;
             src[g] = reinterpret_cast<const uint8_t*>(b) + ((ln & 7) ^ f) * 16;
         }
     }
-    __device__ __forceinline__ void issue_clamped(uint32_t L) const {
+    // Issues the next line of every record, then steps each record's pointer
+    // to its following line while it has one (a record that has run out
+    // re-reads its last line; the data is discarded).  Pointers advance in
+    // place: no per-issue address temporaries next to the line in VGPRs.
+    // All records have the same number of lines: no clamping, no rem[].
+    __device__ __forceinline__ void issue_next_uniform() {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint32_t l = L < lim[g] ? L : lim[g];
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + (uint64_t)l * 128),
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[g],
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
-                                             kLdsAux);
+                                             kGatherAux);
+            src[g] += 128;
+        }
+    }
+    __device__ __forceinline__ void issue_next() {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[g],
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             kGatherAux);
+            const bool more = rem[g] != 0;
+            src[g] += more ? 128 : 0;
+            rem[g] -= more ? 1u : 0u;
         }
     }
 };
@@ -731,13 +809,11 @@ __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p
     return p;
 }
 
+// Last block: w holds the final rem (< kBlock) message bytes, zero filled;
+// appends 0x80, zeros and the length of all `total` bytes (md5.h:266-288 /
+// sha1.h:816-840 / sha2.h:706-742).
 template <class H>
-__device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
-    uint32_t w[H::kWords];
-    const uint64_t nfull = len / H::kBlock;
-    const uint8_t* p = md_full_blocks(st, msg, nfull);
-    const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
-    load_block_tail<H>(p, rem, w);
+__device__ __forceinline__ void md_pad_tail(H& st, uint32_t* w, uint32_t rem, uint64_t total) {
     // 0x80 terminator at byte `rem` (of a 64- or 128-byte block).
 #pragma unroll
     for (int h = 0; h < H::kBlock / 64; ++h)
@@ -747,8 +823,45 @@ __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t l
 #pragma unroll
         for (int k = 0; k < H::kWords; ++k) w[k] = 0u;
     }
-    H::put_length(w, len + prefix);
+    H::put_length(w, total);
     st.compress(w);
+}
+
+template <class H>
+__device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
+    uint32_t w[H::kWords];
+    const uint64_t nfull = len / H::kBlock;
+    const uint8_t* p = md_full_blocks(st, msg, nfull);
+    const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
+    load_block_tail<H>(p, rem, w);
+    md_pad_tail(st, w, rem, len + prefix);
+}
+
+// Whole virtual message A[0, la) || B[0, lb) from state `st` after `prefix`
+// bytes: A's whole blocks straight from A, the block(s) holding the seam
+// assembled word by word, then the rest straight from B (any alignment).
+template <class H>
+__device__ __forceinline__ void md_message2(H& st, const uint8_t* A, uint64_t la, const uint8_t* B, uint64_t lb,
+                                            uint64_t prefix) {
+    const uint64_t nA = la / H::kBlock;
+    md_full_blocks(st, A, nA);
+    uint64_t done = nA * H::kBlock;
+    const uint64_t total = la + lb;
+    uint32_t w[H::kWords];
+    while (done < la && done + H::kBlock <= total) {   // a whole block across the seam
+#pragma unroll
+        for (int h = 0; h < H::kBlock / 64; ++h) load_vblock64(A, la, B, lb, done + 64 * h, w + 16 * h);
+        st.compress(w);
+        done += H::kBlock;
+    }
+    if (done >= la) {                                  // the rest lies in B
+        md_message(st, B + (done - la), total - done, prefix + done);
+        return;
+    }
+    // the final, partial block still holds bytes of A
+#pragma unroll
+    for (int h = 0; h < H::kBlock / 64; ++h) load_vblock64(A, la, B, lb, done + 64 * h, w + 16 * h);
+    md_pad_tail(st, w, (uint32_t)(total - done), total + prefix);
 }
 
 // Final block of a message whose length is a whole number of blocks: 0x80,

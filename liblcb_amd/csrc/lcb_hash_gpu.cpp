@@ -83,10 +83,12 @@ int launch_ordered(int alg, KArgs a, hipStream_t s) {
     // The bucketing permutation holds message indices as uint32.
     if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
-        const size_t bytes = (kLenClasses + a.count) * sizeof(uint32_t);
+        // work: [kLenClasses class cursors | 1 tile-queue head | count order]
+        const size_t bytes = (kLenClasses + 1 + a.count) * sizeof(uint32_t);
         LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&work), bytes, s));
-        launch_bucketing(a.lengths, a.count, work, work + kLenClasses, s);
-        a.order = work + kLenClasses;
+        launch_bucketing(a.lengths, a.count, work, work + kLenClasses + 1, s);
+        a.tile_next = work + kLenClasses;
+        a.order = work + kLenClasses + 1;
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();
@@ -152,14 +154,22 @@ void parallel_copy(const std::vector<Piece>& pieces, size_t bytes) {
 
 namespace lcbgpu {
 
+static void set_keys(KArgs& a, const KeyTable* kt, const uint32_t* index) {
+    if (!kt) return;
+    a.key_mode = kt->mode; a.keys = kt->keys; a.key_off = kt->key_off; a.key_len = kt->key_len;
+    a.nkeys = kt->nkeys; a.mid = kt->mid; a.key_index = index;
+}
+
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init) {
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init,
+                 const KeyTable* kt) {
     KArgs a;
     a.data = data; a.offsets = offsets; a.lengths = lengths; a.order = nullptr;
     a.count = count; a.stride = stride; a.fixed_len = fixed_len; a.digests = digests;
     a.mid = nullptr;
     a.init = init;
+    set_keys(a, kt, kt ? kt->index : nullptr);
     uint32_t* mid = nullptr;
     uint8_t* dkey = nullptr;
     if (key) {
@@ -270,7 +280,8 @@ void stage_release(Stage* st) {
 
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage) {
+               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage,
+               const KeyTable* kt) {
     int dev = 0;
     LCB_TRY(hipGetDevice(&dev));
     Stage& S = stage ? *stage : g_stage;
@@ -345,11 +356,15 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
         KArgs a;
         a.order = nullptr; a.count = n; a.digests = S.d_dig[b]; a.mid = mid;
         bool ok = true;
-        if (init) {  // CRC X_update() values of this chunk
-            memcpy(S.h_init[b], init + i, n * 4);
+        // One uint32 per message rides along with the chunk: the CRC
+        // X_update() values, or the key index of a keyed batch.
+        const uint32_t* per_msg = init ? init : (kt ? kt->index : nullptr);
+        if (per_msg) {
+            memcpy(S.h_init[b], per_msg + i, n * 4);
             ok = hipMemcpyAsync(S.d_init[b], S.h_init[b], n * 4, hipMemcpyHostToDevice, s) == hipSuccess;
-            a.init = S.d_init[b];
+            if (init) a.init = S.d_init[b];
         }
+        set_keys(a, kt, kt && kt->index ? S.d_init[b] : nullptr);
         if (!ok) {
         } else if (direct) {
             ok = hipMemcpyAsync(S.d_data[b], data + base, span ? span : 1, hipMemcpyHostToDevice, s) == hipSuccess;
@@ -452,6 +467,73 @@ int lcb_hash_batch(int alg, const uint8_t* key, size_t key_len, const uint8_t* d
                             digests, reinterpret_cast<hipStream_t>(stream), nullptr);
     return batch_host(alg, key, key_len, data, offsets, lengths, count, stride, fixed_len, digests,
                       nullptr, nullptr);
+}
+
+int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint64_t* key_offsets,
+                         const uint32_t* key_lengths, size_t nkeys, const uint32_t* key_index,
+                         const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, size_t count,
+                         uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags, void* stream) {
+    static_assert(LCB_HASH_KEY_HMAC == kKeyHmac && LCB_HASH_KEY_PREFIX == kKeyPrefix &&
+                  LCB_HASH_KEY_SUFFIX == kKeySuffix, "key mode ids");
+    if (alg < LCB_HASH_MD5 || alg > LCB_HASH_GOST512) return EINVAL;
+    if (key_mode < LCB_HASH_KEY_HMAC || key_mode > LCB_HASH_KEY_SUFFIX) return EINVAL;
+    if (flags & ~LCB_HASH_F_DEVICE) return EINVAL;
+    if (nkeys == 0 || nkeys > UINT32_MAX || !key_lengths) return EINVAL;
+    if (count == 0) return 0;
+    if (!data || !digests) return EINVAL;
+    const bool dev_mode = flags & LCB_HASH_F_DEVICE;
+    // Pack the key table (host memory) into one blob.
+    std::vector<uint32_t> koff(nkeys), klen(nkeys);
+    uint64_t total = 0;
+    for (size_t k = 0; k < nkeys; ++k) {
+        if (key_lengths[k] && !keys) return EINVAL;
+        koff[k] = (uint32_t)total;
+        klen[k] = key_lengths[k];
+        total += key_lengths[k];
+        if (total > UINT32_MAX) return EINVAL;
+    }
+    if (!dev_mode && key_index)
+        for (size_t i = 0; i < count; ++i)
+            if (key_index[i] >= nkeys) return EINVAL;
+    if (int rc = ensure_init()) return rc;
+    std::vector<uint8_t> blob(total ? total : 1);
+    for (size_t k = 0; k < nkeys; ++k)
+        if (klen[k]) memcpy(blob.data() + koff[k], keys + (key_offsets ? key_offsets[k] : 0), klen[k]);
+    hipStream_t s = dev_mode ? reinterpret_cast<hipStream_t>(stream) : nullptr;
+    const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = nkeys * 4;
+    const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
+    uint8_t* dbuf = nullptr;
+    LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b, s));
+    KeyTable kt;
+    kt.mode = (uint32_t)key_mode;
+    kt.keys = dbuf;
+    kt.key_off = reinterpret_cast<const uint32_t*>(dbuf + blob_b);
+    kt.key_len = reinterpret_cast<const uint32_t*>(dbuf + blob_b + tab_b);
+    kt.nkeys = (uint32_t)nkeys;
+    kt.mid = reinterpret_cast<const uint32_t*>(dbuf + blob_b + 2 * tab_b);
+    kt.index = key_index;
+    int rc = 0;
+    // The table's host vectors die on return: copy, then wait for the copies.
+    if (hipMemcpyAsync(dbuf, blob.data(), blob.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dbuf + blob_b, koff.data(), tab_b, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dbuf + blob_b + tab_b, klen.data(), tab_b, hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = EIO;
+    if (!rc && key_mode != LCB_HASH_KEY_SUFFIX) {
+        KArgs a;
+        a.key_mode = kt.mode; a.keys = kt.keys; a.key_off = kt.key_off; a.key_len = kt.key_len; a.nkeys = kt.nkeys;
+        launch_key_prep(alg, a, const_cast<uint32_t*>(kt.mid), s);
+        rc = map_err(hipGetLastError());
+    }
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EIO;
+    if (!rc) {
+        rc = dev_mode ? batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s,
+                                     nullptr, &kt)
+                      : batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
+                                   nullptr, nullptr, &kt);
+    }
+    (void)hipFreeAsync(dbuf, s);
+    if (!dev_mode) (void)hipStreamSynchronize(s);
+    return rc;
 }
 
 int md5_get_digest_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,

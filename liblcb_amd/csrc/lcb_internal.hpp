@@ -19,7 +19,23 @@ struct KArgs {
     uint8_t* digests;          // packed count x D (CRC: count x uint32)
     const uint32_t* mid;       // HMAC mid-states (nullptr: plain digest)
     const uint32_t* init = nullptr;  // CRC: per-buffer X_update() value (nullptr: one-shot X())
+    uint32_t* tile_next = nullptr;   // bucketed batches: work-queue head of md_tiles_kernel (zeroed)
+    // Keyed batches (lcb_hash_batch_keyed): per-message key index into a key
+    // table on the device; `mid` then holds 2 * kMidWords words per key.
+    uint32_t key_mode = 0;           // kKeyNone / kKeyHmac / kKeyPrefix / kKeySuffix
+    const uint32_t* key_index = nullptr;  // nullptr: key 0 for every message
+    const uint8_t* keys = nullptr;   // key bytes
+    const uint32_t* key_off = nullptr;
+    const uint32_t* key_len = nullptr;
+    uint32_t nkeys = 0;
 };
+
+// KArgs::key_mode.  kKeyNone: plain digest, or single-key HMAC when mid is
+// set (lcb_hash_batch).  The others take key k = key_index[i]:
+//   kKeyHmac    HMAC(K_k, m_i)            mid[k]: states after K^ipad, K^opad
+//   kKeyPrefix  H(K_k || m_i)             mid[k]: state after K_k's whole blocks
+//   kKeySuffix  H(m_i || K_k)
+enum { kKeyNone = 0, kKeyHmac = 1, kKeyPrefix = 2, kKeySuffix = 3 };
 
 // Fixed-stride batch of 16-B aligned records with at least one whole 128-B
 // line each: the shape the LDS-DMA line-stream kernels accept.
@@ -78,6 +94,8 @@ void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, u
                       hipStream_t s);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
                       uint32_t* mid, hipStream_t s);
+// Key-table prep of a keyed batch: mid[k] for every key (kKeyHmac, kKeyPrefix).
+void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s);
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
 void gost_table_host(uint64_t* out);
 
@@ -99,12 +117,25 @@ int launch_ordered(int alg, KArgs a, hipStream_t s);
 // (nullptr: the calling thread's own staging context).  `init`: CRC
 // X_update() values (nullptr otherwise).
 struct Stage;
+// Key table of a keyed batch on the device (lcb_hash_batch_keyed), with the
+// per-message key index kept where the caller gave it.
+struct KeyTable {
+    uint32_t mode = 0;                 // kKeyHmac / kKeyPrefix / kKeySuffix
+    const uint8_t* keys = nullptr;     // device: packed key bytes
+    const uint32_t* key_off = nullptr; // device
+    const uint32_t* key_len = nullptr; // device
+    uint32_t nkeys = 0;
+    const uint32_t* mid = nullptr;     // device: 2 * kMidWords words per key
+    const uint32_t* index = nullptr;   // per message (device or host memory, as the batch), or nullptr
+};
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init);
+                 uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init,
+                 const KeyTable* kt = nullptr);
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
-               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage);
+               uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage,
+               const KeyTable* kt = nullptr);
 Stage* stage_acquire(int dev);      // pooled staging context (multi-device workers)
 void stage_release(Stage* st);
 

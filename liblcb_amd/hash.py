@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (ALG_IDS, DIGEST_SIZE, F_COPY_PARTS, F_DEVICE, GOST256, GOST512, MD5, SHA1, SHA224,
+from ._lib import (ALG_IDS, DIGEST_SIZE, F_COPY_PARTS, F_DEVICE, GOST256, KEY_HMAC, KEY_PREFIX, KEY_SUFFIX, GOST512, MD5, SHA1, SHA224,
                    SHA256, SHA384, SHA512, check, lib)
 
 __all__ = [
@@ -27,7 +27,7 @@ __all__ = [
     "sha1_get_digest_batch", "sha1_hmac_get_digest_batch", "sha2_get_digest_batch",
     "sha2_hmac_get_digest_batch", "gost3411_2012_get_digest_batch",
     "gost3411_2012_hmac_get_digest_batch", "gen_synthetic", "sha2_alg", "gost_alg",
-    "partition", "hash_batch_multi",
+    "partition", "hash_batch_multi", "hash_batch_keyed", "KEY_HMAC", "KEY_PREFIX", "KEY_SUFFIX",
 ]
 
 
@@ -262,4 +262,63 @@ def hash_batch_multi(devs, alg, data, *, offsets=None, lengths=None, count=None,
                                      offsets.ctypes.data if offsets is not None else None,
                                      lengths.ctypes.data if lengths is not None else None,
                                      count, stride, fixed_len, out.ctypes.data, 0))
+    return out
+
+
+def hash_batch_keyed(alg, mode, keys, data, *, key_index=None, offsets=None, lengths=None, count=None,
+                     stride=None, fixed_len=None, out=None):
+    """lcb_hash_batch_keyed: message i hashed with key keys[key_index[i]]
+    (key 0 without key_index) as HMAC(K, m) (KEY_HMAC), H(K || m)
+    (KEY_PREFIX) or H(m || K) (KEY_SUFFIX) — the RADIUS shapes
+    (include/proto/radius.h:745-919, 1315-1377).  keys: sequence of bytes.
+    key_index lives with the batch: a device tensor in device mode."""
+    if isinstance(alg, str):
+        alg = ALG_IDS[alg]
+    D = DIGEST_SIZE[alg]
+    keys = [bytes(k) for k in keys]
+    blob = np.frombuffer(b"".join(keys) or b"\0", np.uint8)
+    klen = np.array([len(k) for k in keys], np.uint32)
+    koff = np.zeros(len(keys), np.uint64)
+    if len(keys) > 1:
+        koff[1:] = np.cumsum(klen[:-1], dtype=np.uint64)
+    L = lib()
+    if _is_dev(data):
+        assert data.dtype == torch.uint8 and data.is_contiguous()
+        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
+        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
+        if key_index is not None:
+            assert _is_dev(key_index) and key_index.dtype in (torch.int32, torch.uint32) and \
+                key_index.numel() >= count and key_index.is_contiguous()
+        if out is None:
+            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+        with torch.cuda.device(data.device):
+            stream = torch.cuda.current_stream(data.device).cuda_stream
+            check(L.lcb_hash_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data,
+                                         len(keys), key_index.data_ptr() if key_index is not None else None,
+                                         data.data_ptr(), offsets.data_ptr() if offsets is not None else None,
+                                         lengths.data_ptr() if lengths is not None else None,
+                                         count, stride, fixed_len, out.data_ptr(), F_DEVICE, stream))
+        return out
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        data = np.frombuffer(bytes(data), dtype=np.uint8)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    nbytes = data.size
+    if data.size == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
+    if key_index is not None:
+        key_index = np.ascontiguousarray(key_index, dtype=np.uint32)
+        assert key_index.size >= count
+    if out is None:
+        out = np.empty((count, D), dtype=np.uint8)
+    check(L.lcb_hash_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data, len(keys),
+                                 key_index.ctypes.data if key_index is not None else None, data.ctypes.data,
+                                 offsets.ctypes.data if offsets is not None else None,
+                                 lengths.ctypes.data if lengths is not None else None,
+                                 count, stride, fixed_len, out.ctypes.data, 0, None))
     return out

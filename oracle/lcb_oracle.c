@@ -466,6 +466,38 @@ int or_batch(int alg, const uint8_t *key, size_t key_len,
 	return 0;
 }
 
+/* Keyed batches (lcb_hash_batch_keyed): message i with key k = key_index[i]
+ * (NULL: 0) of the table keys + key_offsets[k] (NULL: 0), key_lengths[k]:
+ *   mode 1  HMAC(K, m)                 radius.h:850-919 (hmac_md5_*)
+ *   mode 2  H(K || m)                  radius.h:774-789 (md5_update(key) then
+ *                                      (authenticator | c_j) from a ctx copy)
+ *   mode 3  H(m || K)                  radius.h:1331-1336, 1346-1352 */
+int or_batch_keyed(int alg, int mode, const uint8_t *keys, const uint64_t *key_offsets,
+    const uint32_t *key_lengths, size_t nkeys, const uint32_t *key_index,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+    size_t count, uint64_t stride, uint32_t fixed_len, uint8_t *digests) {
+	size_t ds = or_digest_size(alg);
+	if (ds == 0 || nkeys == 0 || mode < 1 || mode > 3) return -1;
+	for (size_t i = 0; i < count; i++) {
+		const uint8_t *p = base + (offsets ? offsets[i] : (uint64_t)i * stride);
+		size_t n = lengths ? lengths[i] : fixed_len;
+		size_t k = key_index ? key_index[i] : 0;
+		if (k >= nkeys) return -1;
+		const uint8_t *K = keys + (key_offsets ? key_offsets[k] : 0);
+		size_t kl = key_lengths[k];
+		or_ctx_t c;
+		if (mode == 1) {
+			or_hmac(alg, K, kl, p, n, digests + i * ds);
+			continue;
+		}
+		or_init(&c, alg);
+		if (mode == 2) { or_update(&c, K, kl); or_update(&c, p, n); }
+		else { or_update(&c, p, n); or_update(&c, K, kl); }
+		or_final(&c, digests + i * ds);
+	}
+	return 0;
+}
+
 /* ------------------------------------------------- synthetic input */
 uint64_t or_mix64(uint64_t x) {
 	uint64_t z = x + 0x9e3779b97f4a7c15ull;

@@ -62,6 +62,13 @@ int or_batch(int alg, const uint8_t *key, size_t key_len,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
     size_t count, uint64_t stride, uint32_t fixed_len, uint8_t *digests);
 
+/* Keyed batches, as lcb_hash_batch_keyed: mode 1 HMAC(K, m), 2 H(K || m),
+ * 3 H(m || K) with K = key key_index[i] (NULL: key 0); -1 on a bad index. */
+int or_batch_keyed(int alg, int mode, const uint8_t *keys, const uint64_t *key_offsets,
+    const uint32_t *key_lengths, size_t nkeys, const uint32_t *key_index,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+    size_t count, uint64_t stride, uint32_t fixed_len, uint8_t *digests);
+
 /*
  * CRC-32 family of include/math/crc32.h (oracle/crc32_oracle.c).  Variant
  * ids are shared with include/lcb_crc32_gpu.h.

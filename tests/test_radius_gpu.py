@@ -1,0 +1,214 @@
+"""Keyed batches (lcb_hash_batch_keyed) and the RADIUS shapes built on them.
+
+GPU, against the oracle: every algorithm x {HMAC, H(K || m), H(m || K)}
+with a per-message key index into a 7-key table (key lengths 0, 1, 15, 64,
+65, 128, 200: empty, short, one block, multi-block, longer than the HMAC
+block), ragged misaligned messages of 0..300 bytes, device and host mode.
+
+GPU, against the REFERENCE: tests/golden/radius.json holds 481 packets the
+reference's own radius.h built and signed (radius_pkt_sign) and verified
+(radius_pkt_verify), plus its User-Password encodings.  liblcb_amd.radius
+re-signs the unsigned packets and verifies the signed ones with every MD5 /
+HMAC-MD5 on the GPU: byte-identical packets, identical verification results,
+and tampered packets rejected.
+"""
+import errno
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.pyoracle import gen_stream
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "radius.json")
+KEYS = [b"", b"k", bytes(range(15)), bytes(range(64)), bytes(range(1, 66)), bytes(range(128)),
+        bytes((3 * i) & 0xFF for i in range(200))]
+
+
+@pytest.fixture(scope="module")
+def rad():
+    j = json.load(open(GOLDEN))
+    j["secrets"] = [bytes.fromhex(s) for s in j["secrets"]]
+    return j
+
+
+def _ragged(seed, n):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 301, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    pos = 1
+    for i in range(n):
+        offs[i] = pos
+        pos += int(lens[i]) + int(rng.integers(0, 7))
+    kidx = rng.integers(0, len(KEYS), n).astype(np.uint32)
+    return gen_stream(seed, pos + 8), offs, lens, kidx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_keyed_vs_oracle_device(gpu, oracle, mode):
+    import torch
+    data, offs, lens, kidx = _ragged(10 + mode, 3000)
+    dd = torch.as_tensor(data, device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    dk = torch.as_tensor(kidx.astype(np.int32), device="cuda")
+    for alg in range(1, 9):
+        got = gpu.hash_batch_keyed(alg, mode, KEYS, dd, key_index=dk, offsets=do, lengths=dl).cpu().numpy()
+        exp = oracle.batch_keyed(alg, mode, KEYS, data, kidx, offs, lens)
+        assert np.array_equal(got, exp), (alg, mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_keyed_vs_oracle_host_and_fixed(gpu, oracle, mode):
+    data, offs, lens, kidx = _ragged(20 + mode, 6000)   # above the bucketing threshold
+    for alg in (1, 2, 4, 6, 7):
+        got = gpu.hash_batch_keyed(alg, mode, KEYS, data, key_index=kidx, offsets=offs, lengths=lens)
+        assert np.array_equal(got, oracle.batch_keyed(alg, mode, KEYS, data, kidx, offs, lens)), (alg, mode)
+    # fixed stride, one key for every message (key_index NULL)
+    fx = gen_stream(30 + mode, 500 * 200)
+    for alg in (1, 5, 8):
+        got = gpu.hash_batch_keyed(alg, mode, [KEYS[4]], fx, count=500, stride=200, fixed_len=190)
+        exp = oracle.batch_keyed(alg, mode, [KEYS[4]], fx, None, count=500, stride=200, fixed_len=190)
+        assert np.array_equal(got, exp), (alg, mode)
+
+
+@pytest.mark.gpu
+def test_keyed_hmac_equals_single_key_hmac(gpu):
+    """KEY_HMAC with one key == the single-key HMAC of lcb_hash_batch."""
+    import torch
+    data = gpu.gen_synthetic(3, 4096 * 1024)
+    for alg in (1, 4, 7):
+        a = gpu.hash_batch(alg, data, count=4096, stride=1024, fixed_len=1024, key=b"radius-secret")
+        b = gpu.hash_batch_keyed(alg, gpu.KEY_HMAC, [b"radius-secret"], data, count=4096, stride=1024,
+                                 fixed_len=1024)
+        assert bool((a == b).all()), alg
+        torch.cuda.synchronize()
+
+
+def test_keyed_argument_errors():
+    import liblcb_amd
+    try:
+        L = liblcb_amd.lib()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    buf = np.zeros(64, np.uint8)
+    out = np.zeros(64, np.uint8)
+    kl = np.array([4], np.uint32)
+    k = np.frombuffer(b"abcd", np.uint8)
+    args = (k.ctypes.data, None, kl.ctypes.data, 1, None, buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 0,
+            None)
+    assert L.lcb_hash_batch_keyed(1, 0, *args) == errno.EINVAL          # mode
+    assert L.lcb_hash_batch_keyed(1, 4, *args) == errno.EINVAL
+    assert L.lcb_hash_batch_keyed(9, 1, *args) == errno.EINVAL          # alg
+    assert L.lcb_hash_batch_keyed(1, 1, k.ctypes.data, None, kl.ctypes.data, 0, None, buf.ctypes.data, None, None,
+                                  1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL   # no keys
+    assert L.lcb_hash_batch_keyed(1, 1, None, None, kl.ctypes.data, 1, None, buf.ctypes.data, None, None,
+                                  1, 0, 8, out.ctypes.data, 0, None) == errno.EINVAL   # key bytes missing
+    bad = np.array([1], np.uint32)                                         # index >= nkeys (host mode)
+    import torch
+    if not torch.cuda.is_available():
+        assert L.lcb_hash_batch_keyed(1, 1, k.ctypes.data, None, kl.ctypes.data, 1, bad.ctypes.data,
+                                      buf.ctypes.data, None, None, 1, 0, 8, out.ctypes.data, 0, None) == \
+            errno.EINVAL
+
+
+# ----------------------------------------------------------------- RADIUS
+@pytest.mark.gpu
+@pytest.mark.parametrize("device", [False, True])
+def test_sign_matches_reference(gpu, rad, device):
+    from liblcb_amd.radius import radius_pkt_sign_batch
+    P = rad["packets"]
+    got = radius_pkt_sign_batch([bytes.fromhex(p["pre"]) for p in P], rad["secrets"],
+                                [p["key"] for p in P], device=device)
+    bad = [i for i, p in enumerate(P) if got[i].hex() != p["signed"]]
+    assert not bad, (len(bad), [P[i]["code"] for i in bad[:10]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device", [False, True])
+def test_verify_matches_reference(gpu, rad, device):
+    from liblcb_amd.radius import radius_pkt_verify_batch
+    P = rad["packets"]
+    reqs = [bytes.fromhex(p["request"]) if p["kind"] == "reply" else None for p in P]
+    err, out = radius_pkt_verify_batch([bytes.fromhex(p["signed"]) for p in P], rad["secrets"],
+                                       [p["key"] for p in P], reqs, device=device)
+    assert err.tolist() == [0] * len(P)
+    assert [o.hex() for o in out] == [p["verified"] for p in P]
+    # passwords decoded back to the plaintext the reference encoded
+    n = 0
+    for p, o in zip(P, out):
+        if p["kind"] == "request" and p.get("password"):
+            pw = bytes.fromhex(p["password"])
+            from liblcb_amd.radius import find_attr
+            a = find_attr(o, 2)
+            assert o[a + 2:a + 2 + len(pw)] == pw
+            n += 1
+    assert n > 50
+
+
+@pytest.mark.gpu
+def test_verify_rejects_tampering(gpu, rad):
+    """One flipped byte in a signed packet (attribute data, or the
+    authenticator) makes the check the reference would fail fail here."""
+    from liblcb_amd.radius import RANDOM_AUTH, find_attr, radius_pkt_verify_batch
+    P = [p for p in rad["packets"] if p["msg_authr"] or p["code"] not in RANDOM_AUTH]
+    pk, reqs = [], []
+    for p in P:
+        b = bytearray.fromhex(p["signed"])
+        if p["msg_authr"]:
+            b[find_attr(b, 80) + 5] ^= 1            # inside the Message-Authenticator
+        else:
+            b[7] ^= 1                               # inside the authenticator
+        pk.append(bytes(b))
+        reqs.append(bytes.fromhex(p["request"]) if p["kind"] == "reply" else None)
+    err, _ = radius_pkt_verify_batch(pk, rad["secrets"], [p["key"] for p in P], reqs)
+    assert (err == errno.EBADMSG).all(), np.unique(err)
+
+
+@pytest.mark.gpu
+def test_password_encode_vectors(gpu, rad):
+    """radius_pkt_attr_password_encode (radius.h:745-790) for every password
+    length 1..128 through the KEY_PREFIX chain."""
+    from liblcb_amd.radius import radius_pkt_sign_batch
+    pk, ki, want = [], [], []
+    for v in rad["password_encode"]:
+        pw = bytes.fromhex(v["password"])
+        tm = (len(pw) + 15) // 16 * 16
+        attr = bytes([2, 2 + tm]) + pw + bytes(tm - len(pw))
+        hdr = bytes([1, 0]) + (20 + len(attr)).to_bytes(2, "big") + bytes.fromhex(v["authenticator"])
+        pk.append(hdr + attr)
+        ki.append(v["key"])
+        want.append(v["encoded"])
+    got = radius_pkt_sign_batch(pk, rad["secrets"], ki)
+    assert [g[22:].hex() for g in got] == want
+
+
+# ------------------------------------------- host logic, CPU (oracle backend)
+@pytest.fixture
+def oracle_keyed(monkeypatch, oracle):
+    """liblcb_amd.radius with its keyed batches served by the oracle: checks
+    the host-side packet logic (field substitution, chaining, XOR) on CPU."""
+    import liblcb_amd.radius as R
+
+    def fake(alg, mode, keys, data, key_index=None, offsets=None, lengths=None, **kw):
+        return oracle.batch_keyed(alg, mode, keys, data, key_index, offsets, lengths)
+    monkeypatch.setattr(R, "hash_batch_keyed", fake)
+    return R
+
+
+def test_radius_host_logic_sign_verify(oracle_keyed, rad):
+    R = oracle_keyed
+    P = rad["packets"]
+    got = R.radius_pkt_sign_batch([bytes.fromhex(p["pre"]) for p in P], rad["secrets"], [p["key"] for p in P])
+    assert [g.hex() for g in got] == [p["signed"] for p in P]
+    reqs = [bytes.fromhex(p["request"]) if p["kind"] == "reply" else None for p in P]
+    err, out = R.radius_pkt_verify_batch(got, rad["secrets"], [p["key"] for p in P], reqs)
+    assert err.tolist() == [0] * len(P)
+    assert [o.hex() for o in out] == [p["verified"] for p in P]
+    # a reply without its request: EINVAL, as radius_pkt_verify returns
+    i = [k for k, p in enumerate(P) if p["kind"] == "reply" and p["code"] in R.REPLY_AUTH][0]
+    err, _ = R.radius_pkt_verify_batch([got[i]], rad["secrets"], [P[i]["key"]], [None])
+    assert err.tolist() == [errno.EINVAL]
