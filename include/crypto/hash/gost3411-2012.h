@@ -7,9 +7,9 @@
  * gost3411_2012_init(bits, ctx) with 256|32 -> 256-bit and ANY other value
  * -> 512-bit, exactly as the reference.
  *
- * The LPS lookup table (8 x 256 x u64) is not spelled out in the source: it is
- * generated once per translation unit from the S-box pi and the linear map A
- * on first use (thread-safe), so the header stays small.  Portable C only:
+ * The LPS lookup table (8 x 256 x u64) is read-only data generated from the
+ * S-box pi and the linear map A (gost3411-2012-lps.h, tools/gen_gost_table.py):
+ * no mutable global, as the reference.  Portable C only:
  * the use_sse/use_avx fields exist for source compatibility and are ignored.
  * One-message CPU path; batches go through include/lcb_hash_gpu.h.
  */
@@ -40,64 +40,30 @@
 #define GOST3411_2012_MSG_BLK_64CNT	(GOST3411_2012_MSG_BLK_SIZE / sizeof(uint64_t))
 #define GOST3411_2012_ROUNDS_COUNT	((size_t)12)
 
+#define GOST3411_2012_ALIGN(__n) __attribute__ ((aligned(__n)))
+
+/* Field for field the reference's layout (gost3411-2012.h:953-965), so
+ * sizeof / offsetof agree (tests/test_dropin_headers.py). */
 typedef struct gost3411_2012_ctx_s {
 	size_t hash_size;	/* 32 or 64 */
 	size_t buffer_usage;	/* bytes in buffer, always < 64 between calls */
 	int use_sse;		/* source compatibility only */
 	int use_avx;		/* source compatibility only */
-	uint64_t hash[GOST3411_2012_HASH_MAX_64CNT];	/* h */
-	uint64_t counter[GOST3411_2012_MSG_BLK_64CNT];	/* N: bits processed */
-	uint64_t sigma[GOST3411_2012_MSG_BLK_64CNT];	/* Sigma: sum of blocks */
-	uint64_t buffer[GOST3411_2012_MSG_BLK_64CNT];	/* partial block */
+	GOST3411_2012_ALIGN(32) uint64_t hash[GOST3411_2012_HASH_MAX_64CNT];	/* h */
+	GOST3411_2012_ALIGN(32) uint64_t counter[GOST3411_2012_MSG_BLK_64CNT];	/* N: bits processed */
+	GOST3411_2012_ALIGN(32) uint64_t sigma[GOST3411_2012_MSG_BLK_64CNT];	/* Sigma: sum of blocks */
+	GOST3411_2012_ALIGN(32) uint64_t buffer[GOST3411_2012_MSG_BLK_64CNT];	/* partial block */
+	GOST3411_2012_ALIGN(8) uint64_t kbuf[GOST3411_2012_MSG_BLK_64CNT];	/* layout only */
+	GOST3411_2012_ALIGN(8) uint64_t tbuf[GOST3411_2012_MSG_BLK_64CNT];	/* layout only */
+	GOST3411_2012_ALIGN(8) uint64_t sbuf[GOST3411_2012_MSG_BLK_64CNT];	/* layout only */
 } gost3411_2012_ctx_t, *gost3411_2012_ctx_p;
 
 typedef struct hmac_gost3411_2012_ctx_s {
 	gost3411_2012_ctx_t ctx;
-	uint64_t k_opad[GOST3411_2012_MSG_BLK_64CNT];
+	GOST3411_2012_ALIGN(32) uint64_t k_opad[GOST3411_2012_MSG_BLK_64CNT];
 } hmac_gost3411_2012_ctx_t, *hmac_gost3411_2012_ctx_p;
 
 static void *(*volatile gost3411_2012_wipe_fn)(void *, int, size_t) = memset;
-
-/* RFC 6986 section 6.1: pi. */
-static const uint8_t gost3411_2012_pi[256] = {
-	252, 238, 221,  17, 207, 110,  49,  22, 251, 196, 250, 218,  35, 197,   4,  77,
-	233, 119, 240, 219, 147,  46, 153, 186,  23,  54, 241, 187,  20, 205,  95, 193,
-	249,  24, 101,  90, 226,  92, 239,  33, 129,  28,  60,  66, 139,   1, 142,  79,
-	  5, 132,   2, 174, 227, 106, 143, 160,   6,  11, 237, 152, 127, 212, 211,  31,
-	235,  52,  44,  81, 234, 200,  72, 171, 242,  42, 104, 162, 253,  58, 206, 204,
-	181, 112,  14,  86,   8,  12, 118,  18, 191, 114,  19,  71, 156, 183,  93, 135,
-	 21, 161, 150,  41,  16, 123, 154, 199, 243, 145, 120, 111, 157, 158, 178, 177,
-	 50, 117,  25,  61, 255,  53, 138, 126, 109,  84, 198, 128, 195, 189,  13,  87,
-	223, 245,  36, 169,  62, 168,  67, 201, 215, 121, 214, 246, 124,  34, 185,   3,
-	224,  15, 236, 222, 122, 148, 176, 188, 220, 232,  40,  80,  78,  51,  10,  74,
-	167, 151,  96, 115,  30,   0,  98,  68,  26, 184,  56, 130, 100, 159,  38,  65,
-	173,  69,  70, 146,  39,  94,  85,  47, 140, 163, 165, 125, 105, 213, 149,  59,
-	  7,  88, 179,  64, 134, 172,  29, 247,  48,  55, 107, 228, 136, 217, 231, 137,
-	225,  27, 131,  73,  76,  63, 248, 254, 141,  83, 170, 144, 202, 216, 133,  97,
-	 32, 113, 103, 164,  45,  43,   9,  91, 203, 155,  37, 208, 190, 229, 108,  82,
-	 89, 166, 116, 210, 230, 244, 180, 192, 209, 102, 175, 194,  57,  75,  99, 182
-};
-
-/* RFC 6986 section 6.3: the linear transformation l, one row per input bit
- * (row 0 = most significant bit of a 64-bit word). */
-static const uint64_t gost3411_2012_Arow[64] = {
-	0x8e20faa72ba0b470ull, 0x47107ddd9b505a38ull, 0xad08b0e0c3282d1cull, 0xd8045870ef14980eull,
-	0x6c022c38f90a4c07ull, 0x3601161cf205268dull, 0x1b8e0b0e798c13c8ull, 0x83478b07b2468764ull,
-	0xa011d380818e8f40ull, 0x5086e740ce47c920ull, 0x2843fd2067adea10ull, 0x14aff010bdd87508ull,
-	0x0ad97808d06cb404ull, 0x05e23c0468365a02ull, 0x8c711e02341b2d01ull, 0x46b60f011a83988eull,
-	0x90dab52a387ae76full, 0x486dd4151c3dfdb9ull, 0x24b86a840e90f0d2ull, 0x125c354207487869ull,
-	0x092e94218d243cbaull, 0x8a174a9ec8121e5dull, 0x4585254f64090fa0ull, 0xaccc9ca9328a8950ull,
-	0x9d4df05d5f661451ull, 0xc0a878a0a1330aa6ull, 0x60543c50de970553ull, 0x302a1e286fc58ca7ull,
-	0x18150f14b9ec46ddull, 0x0c84890ad27623e0ull, 0x0642ca05693b9f70ull, 0x0321658cba93c138ull,
-	0x86275df09ce8aaa8ull, 0x439da0784e745554ull, 0xafc0503c273aa42aull, 0xd960281e9d1d5215ull,
-	0xe230140fc0802984ull, 0x71180a8960409a42ull, 0xb60c05ca30204d21ull, 0x5b068c651810a89eull,
-	0x456c34887a3805b9ull, 0xac361a443d1c8cd2ull, 0x561b0d22900e4669ull, 0x2b838811480723baull,
-	0x9bcf4486248d9f5dull, 0xc3e9224312c8c1a0ull, 0xeffa11af0964ee50ull, 0xf97d86d98a327728ull,
-	0xe4fa2054a80b329cull, 0x727d102a548b194eull, 0x39b008152acb8227ull, 0x9258048415eb419dull,
-	0x492c024284fbaec0ull, 0xaa16012142f35760ull, 0x550b8e9e21f7a530ull, 0xa48b474f9ef5dc18ull,
-	0x70a6a56e2440598eull, 0x3853dc371220a247ull, 0x1ca76e95091051adull, 0x0edd37c48a08a6d8ull,
-	0x07e095624504536cull, 0x8d70c431ac02a736ull, 0xc83862965601dd1bull, 0x641c314b2b8ee083ull
-};
 
 /* RFC 6986 section 6.4: iteration constants C_1..C_12 (little-endian words). */
 static const uint64_t gost3411_2012_C[GOST3411_2012_ROUNDS_COUNT][GOST3411_2012_MSG_BLK_64CNT] = {
@@ -127,37 +93,9 @@ static const uint64_t gost3411_2012_C[GOST3411_2012_ROUNDS_COUNT][GOST3411_2012_
 	  0xf82012d430219f9bull, 0xcda43c32bcdf1d77ull, 0xd21380b00449b17aull, 0x378ee767f11631baull }
 };
 
-/* LPS table: T[j][b] = L(pi[b] in byte j) — generated on first use. */
-static uint64_t gost3411_2012_T[8][256];
-static int gost3411_2012_T_state;	/* 0 empty, 1 building, 2 ready */
-
-static inline void
-gost3411_2012_tables(void) {
-	int expect = 0;
-	size_t j, b, s;
-	uint64_t v;
-
-	if (2 == __atomic_load_n(&gost3411_2012_T_state, __ATOMIC_ACQUIRE))
-		return;
-	if (__atomic_compare_exchange_n(&gost3411_2012_T_state, &expect, 1, 0,
-	    __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-		for (j = 0; j < 8; j ++) {
-			for (b = 0; b < 256; b ++) {
-				v = 0;
-				for (s = 0; s < 8; s ++) {
-					if ((gost3411_2012_pi[b] >> s) & 1) {
-						v ^= gost3411_2012_Arow[63 - 8 * j - s];
-					}
-				}
-				gost3411_2012_T[j][b] = v;
-			}
-		}
-		__atomic_store_n(&gost3411_2012_T_state, 2, __ATOMIC_RELEASE);
-		return;
-	}
-	while (2 != __atomic_load_n(&gost3411_2012_T_state, __ATOMIC_ACQUIRE))
-		;	/* another thread is building the table (microseconds) */
-}
+/* LPS table: T[j][b] = L(pi[b] in byte j), generated from RFC 6986 pi / A by
+ * tools/gen_gost_table.py into read-only data. */
+#include "gost3411-2012-lps.h"
 
 /* dst = LPS(a ^ b); dst may alias a or b. */
 static inline void
@@ -168,8 +106,10 @@ gost3411_2012_xlps(uint64_t *dst, const uint64_t *a, const uint64_t *b) {
 	for (j = 0; j < 8; j ++) {
 		x[j] = (a[j] ^ b[j]);
 	}
+#pragma GCC unroll 8
 	for (i = 0; i < 8; i ++) {
 		r[i] = 0;
+#pragma GCC unroll 8
 		for (j = 0; j < 8; j ++) {
 			r[i] ^= gost3411_2012_T[j][(x[j] >> (8 * i)) & 0xff];
 		}
@@ -249,7 +189,6 @@ gost3411_2012_transform_1(gost3411_2012_ctx_p ctx, const uint64_t *block) {
 static inline void
 gost3411_2012_init(const size_t bits, gost3411_2012_ctx_p ctx) {
 
-	gost3411_2012_tables();
 	memset(ctx, 0x00, sizeof(gost3411_2012_ctx_t));
 	if (256 == bits || GOST3411_2012_256_HASH_SIZE == bits) {
 		ctx->hash_size = GOST3411_2012_256_HASH_SIZE;

@@ -80,19 +80,25 @@ md5_transform(md5_ctx_p ctx, const uint8_t *block) {
 		    ((uint32_t)block[4 * i + 2] << 16) | ((uint32_t)block[4 * i + 3] << 24);
 	}
 	memcpy(v, ctx->hash, sizeof(v));
-	for (i = 0; i < 64; i ++) {
-		switch (i >> 4) {
-		case 0: f = (v[3] ^ (v[1] & (v[2] ^ v[3]))); g = i; break;
-		case 1: f = (v[2] ^ (v[3] & (v[1] ^ v[2]))); g = ((5 * i + 1) & 15); break;
-		case 2: f = (v[1] ^ v[2] ^ v[3]); g = ((3 * i + 5) & 15); break;
-		default: f = (v[2] ^ (v[1] | ~v[3])); g = ((7 * i) & 15); break;
-		}
-		t = v[3];
-		v[3] = v[2];
-		v[2] = v[1];
-		v[1] += md5_rol32((v[0] + f + x[g] + T[i]), S[((i >> 4) << 2) | (i & 3)]);
-		v[0] = t;
-	}
+	/* Four 16-step rounds, each a loop the compiler fully unrolls so the
+	 * word index, constant and rotation fold to immediates. */
+#define MD5_ROUND(__r, __f, __g) do {						\
+	_Pragma("GCC unroll 16")						\
+	for (i = 16 * (__r); i < 16 * (__r) + 16; i ++) {			\
+		f = (__f);							\
+		g = (__g);							\
+		t = v[3];							\
+		v[3] = v[2];							\
+		v[2] = v[1];							\
+		v[1] += md5_rol32((v[0] + f + x[g] + T[i]), S[4 * (__r) + (i & 3)]); \
+		v[0] = t;							\
+	}									\
+} while (0)
+	MD5_ROUND(0, (v[3] ^ (v[1] & (v[2] ^ v[3]))), i);
+	MD5_ROUND(1, (v[2] ^ (v[3] & (v[1] ^ v[2]))), ((5 * i + 1) & 15));
+	MD5_ROUND(2, (v[1] ^ v[2] ^ v[3]), ((3 * i + 5) & 15));
+	MD5_ROUND(3, (v[2] ^ (v[1] | ~v[3])), ((7 * i) & 15));
+#undef MD5_ROUND
 	for (i = 0; i < 4; i ++) {
 		ctx->hash[i] += v[i];
 	}

@@ -27,15 +27,30 @@
 #define SHA1_MSG_BLK_SIZE_MASK	(SHA1_MSG_BLK_SIZE - 1)
 #define SHA1_MSG_BLK_64CNT	(SHA1_MSG_BLK_SIZE / sizeof(uint64_t))
 
+#define SHA1_ALIGN(__n)	__attribute__ ((aligned(__n)))
+#if defined(__SHA__) && defined(__SSSE3__) && defined(__SSE4_1__)
+#	define SHA1_ENABLE_SIMD	1	/* layout only: this header has no SIMD path */
+#endif
+
+/* Field for field the reference's layout (sha1.h:128-139), including the
+ * build-dependent tail, so sizeof / offsetof agree in every build and mixed
+ * translation units see one struct (tests/test_dropin_headers.py). */
 typedef struct sha1_ctx_s {
 	uint64_t count;				/* bytes hashed so far */
-	uint32_t hash[(SHA1_HASH_SIZE / sizeof(uint32_t))];
-	uint64_t buffer[SHA1_MSG_BLK_64CNT];	/* partial block */
+	SHA1_ALIGN(32) uint32_t hash[(SHA1_HASH_SIZE / sizeof(uint32_t))];
+	SHA1_ALIGN(32) uint64_t buffer[SHA1_MSG_BLK_64CNT];	/* partial block */
+	SHA1_ALIGN(32) uint32_t W[80];		/* message schedule scratch */
+#ifdef __SSE2__
+	int use_sse;				/* layout only */
+#endif
+#ifdef SHA1_ENABLE_SIMD
+	int use_simd;				/* layout only */
+#endif
 } sha1_ctx_t, *sha1_ctx_p;
 
 typedef struct hmac_sha1_ctx_s {
 	sha1_ctx_t ctx;
-	uint64_t k_opad[SHA1_MSG_BLK_64CNT];
+	SHA1_ALIGN(32) uint64_t k_opad[SHA1_MSG_BLK_64CNT];
 } hmac_sha1_ctx_t, *hmac_sha1_ctx_p;
 
 static void *(*volatile sha1_wipe_fn)(void *, int, size_t) = memset;
@@ -73,6 +88,7 @@ sha1_transform(sha1_ctx_p ctx, const uint8_t *blocks, const uint8_t *blocks_max)
 		}
 		a = ctx->hash[0]; b = ctx->hash[1]; c = ctx->hash[2];
 		d = ctx->hash[3]; e = ctx->hash[4];
+#pragma GCC unroll 80
 		for (i = 0; i < 80; i ++) {
 			if (i >= 16) {	/* rolling 16-word schedule */
 				w[i & 15] = sha1_rol32((w[(i + 13) & 15] ^ w[(i + 8) & 15] ^

@@ -55,18 +55,29 @@ static const uint64_t SHA2_512_H0[8] = {
 	0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
 	0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull };
 
+#define SHA2_ALIGN(__n)	__attribute__ ((aligned(__n)))
+#if defined(__SHA__) && defined(__SSSE3__) && defined(__SSE4_1__)
+#	define SHA2_ENABLE_SIMD	1	/* layout only: this header has no SIMD path */
+#endif
+
+/* Field for field the reference's layout (sha2.h:152-163), including the
+ * build-dependent tail (tests/test_dropin_headers.py pins sizeof / offsetof). */
 typedef struct sha2_ctx_s {
-	uint64_t hash[(SHA2_HASH_MAX_SIZE / sizeof(uint64_t))]; /* 224/256: 8 x u32 packed */
-	uint64_t buffer[SHA2_MSG_BLK_MAX_64CNT];	/* partial block */
+	SHA2_ALIGN(32) uint64_t hash[(SHA2_HASH_MAX_SIZE / sizeof(uint64_t))]; /* 224/256: 8 x u32 packed */
+	SHA2_ALIGN(32) uint64_t buffer[SHA2_MSG_BLK_MAX_64CNT];	/* partial block */
+	SHA2_ALIGN(32) uint64_t W[80];	/* message schedule scratch */
 	uint64_t count;		/* bytes hashed, low 64 bits */
 	uint64_t count_hi;	/* bytes hashed, high 64 bits */
 	size_t hash_size;	/* 28, 32, 48 or 64 (0: invalid bits) */
 	size_t block_size;	/* 64 or 128 */
+#ifdef SHA2_ENABLE_SIMD
+	int use_simd;		/* layout only */
+#endif
 } sha2_ctx_t, *sha2_ctx_p;
 
 typedef struct hmac_sha2_ctx_s {
 	sha2_ctx_t ctx;
-	uint64_t k_opad[SHA2_MSG_BLK_MAX_64CNT];
+	SHA2_ALIGN(32) uint64_t k_opad[SHA2_MSG_BLK_MAX_64CNT];
 } hmac_sha2_ctx_t, *hmac_sha2_ctx_p;
 
 static void *(*volatile sha2_wipe_fn)(void *, int, size_t) = memset;
@@ -143,6 +154,7 @@ sha2_transform_block64(sha2_ctx_p ctx, const uint8_t *blk) {
 		w[i] = (uint32_t)sha2_load_be(blk + 4 * i, 4);
 	}
 	memcpy(s, h, sizeof(s));
+#pragma GCC unroll 64
 	for (i = 0; i < 64; i ++) {
 		if (i >= 16) {
 			x = w[(i + 1) & 15];	/* W[i-15] */
@@ -155,9 +167,8 @@ sha2_transform_block64(sha2_ctx_p ctx, const uint8_t *blk) {
 		    (s[6] ^ (s[4] & (s[5] ^ s[6]))) + K[i] + w[i & 15]);
 		t2 = ((sha2_ror32(s[0], 2) ^ sha2_ror32(s[0], 13) ^ sha2_ror32(s[0], 22)) +
 		    ((s[0] & s[1]) | (s[2] & (s[0] | s[1]))));
-		memmove(&s[1], &s[0], (7 * sizeof(uint32_t)));
-		s[4] += t1;
-		s[0] = (t1 + t2);
+		s[7] = s[6]; s[6] = s[5]; s[5] = s[4]; s[4] = s[3] + t1;
+		s[3] = s[2]; s[2] = s[1]; s[1] = s[0]; s[0] = (t1 + t2);
 	}
 	for (i = 0; i < 8; i ++) {
 		h[i] += s[i];
@@ -195,6 +206,7 @@ sha2_transform_block128(sha2_ctx_p ctx, const uint8_t *blk) {
 		w[i] = sha2_load_be(blk + 8 * i, 8);
 	}
 	memcpy(s, h, sizeof(s));
+#pragma GCC unroll 80
 	for (i = 0; i < 80; i ++) {
 		if (i >= 16) {
 			x = w[(i + 1) & 15];
@@ -207,9 +219,8 @@ sha2_transform_block128(sha2_ctx_p ctx, const uint8_t *blk) {
 		    (s[6] ^ (s[4] & (s[5] ^ s[6]))) + K[i] + w[i & 15]);
 		t2 = ((sha2_ror64(s[0], 28) ^ sha2_ror64(s[0], 34) ^ sha2_ror64(s[0], 39)) +
 		    ((s[0] & s[1]) | (s[2] & (s[0] | s[1]))));
-		memmove(&s[1], &s[0], (7 * sizeof(uint64_t)));
-		s[4] += t1;
-		s[0] = (t1 + t2);
+		s[7] = s[6]; s[6] = s[5]; s[5] = s[4]; s[4] = s[3] + t1;
+		s[3] = s[2]; s[2] = s[1]; s[1] = s[0]; s[0] = (t1 + t2);
 	}
 	for (i = 0; i < 8; i ++) {
 		h[i] += s[i];

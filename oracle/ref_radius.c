@@ -133,6 +133,28 @@ ref_rad_reply(uint8_t code, const uint8_t *req, const uint8_t *tlv, size_t tlv_l
 	return (0);
 }
 
+/* radius_pkt_sign (radius.h:1487, add_msg_authr = 0) of a copy of an
+ * already built packet `pkt_in`; `out` receives the signed packet. */
+int
+ref_rad_sign(const uint8_t *pkt_in, size_t len, const uint8_t *key, size_t key_len, uint8_t *out,
+    size_t *out_len) {
+	uint8_t buf[RADIUS_PKT_MAX_SIZE];
+	rad_pkt_hdr_p pkt = (rad_pkt_hdr_p)buf;
+	size_t sz = 0;
+	int error;
+
+	if (len > sizeof(buf))
+		return (EINVAL);
+	memset(buf, 0, sizeof(buf));
+	memcpy(buf, pkt_in, len);
+	error = radius_pkt_sign(pkt, sizeof(buf), &sz, (uint8_t*)key, key_len, 0);
+	if (0 != error)
+		return (error);
+	*out_len = RADIUS_PKT_HDR_LEN_GET(pkt);
+	memcpy(out, buf, *out_len);
+	return (0);
+}
+
 /* radius_pkt_chk + radius_pkt_verify (radius.h:1535) of a copy of `pkt`
  * (req may be NULL); `out` receives the packet after verification (User-
  * Password decoded in place).  Returns the reference's result. */

@@ -96,14 +96,76 @@ def test_reference_tests_hash_main_builds_against_dropin(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference sources absent")
-def test_reference_radius_builds_against_dropin(tmp_path):
-    """The only in-tree caller (include/proto/radius.h:53) compiles unchanged,
-    taking crypto/hash/md5.h from this repo (our include dir first)."""
-    exe = str(tmp_path / "radius")
-    subprocess.check_call(["gcc", "-O2", "-w", "-I" + INC, "-I" + os.path.join(REF, "include")] + HAVE +
-                          ["-o", exe, os.path.join(C, "radius_dropin.c")])
-    assert subprocess.run([exe]).returncode == 0
-    # and the preprocessed unit really used our header
+@pytest.mark.parametrize("simd", [False, True])
+def test_ctx_layouts_match_reference(tmp_path, simd):
+    """sizeof / alignment / offsetof of every context struct equal the
+    reference's, in the generic build (as tests/hash) and with SSE4.1 /
+    SHA-NI / AVX2 enabled (the reference's build-dependent fields)."""
+    flags = ["-DLAYOUT_SIMD", "-msse4.1", "-mssse3", "-msha", "-mavx2"] if simd else []
+    outs = []
+    for inc in (os.path.join(REF, "include"), INC):
+        exe = str(tmp_path / ("lay%d" % len(outs)))
+        subprocess.check_call(["gcc", "-O0", "-w"] + flags + ["-I" + inc, "-o", exe, os.path.join(C, "layout.c")])
+        outs.append(subprocess.check_output([exe]).decode())
+    assert outs[0] == outs[1]
+    assert "sha1_ctx_t %d 32" % (480 if simd else 448) in outs[1]
+
+
+def test_gost_table_is_read_only_data():
+    """The drop-in GOST table is static const data (no first-use build, no
+    mutable global): SURVEY.md 8(b) threading contract."""
+    src = open(os.path.join(INC, "crypto", "hash", "gost3411-2012.h")).read()
+    tab = open(os.path.join(INC, "crypto", "hash", "gost3411-2012-lps.h")).read()
+    assert "static const uint64_t gost3411_2012_T[8][256]" in tab
+    assert "__atomic" not in src and "static uint64_t" not in src and "static int" not in src
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference sources absent")
+def test_reference_radius_sign_verify_with_dropin(tmp_path):
+    """The reference's RADIUS code (oracle/ref_radius.c over include/proto/
+    radius.h) built against THIS repo's md5.h signs the packets of
+    tests/golden/radius.json to the same bytes the reference-header build
+    produced, and its radius_pkt_verify accepts them and decodes the same
+    passwords."""
+    import ctypes
+    import json
+    so = str(tmp_path / "libradius_dropin.so")
+    subprocess.check_call(["gcc", "-O2", "-w", "-shared", "-fPIC", "-I" + INC, "-I" + os.path.join(REF, "include")] +
+                          HAVE + ["-o", so, os.path.join(ROOT, "oracle", "ref_radius.c")])
     pp = subprocess.check_output(["gcc", "-E", "-I" + INC, "-I" + os.path.join(REF, "include")] + HAVE +
-                                 [os.path.join(C, "radius_dropin.c")]).decode()
+                                 [os.path.join(ROOT, "oracle", "ref_radius.c")]).decode()
     assert os.path.join(INC, "crypto/hash/md5.h") in pp
+    L = ctypes.CDLL(so)
+    sz = ctypes.c_size_t
+    L.ref_rad_verify.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.c_void_p]
+    L.ref_rad_authenticator_calc.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.c_int,
+                                             ctypes.c_char_p, ctypes.c_void_p]
+    L.ref_rad_msg_authenticator_calc.argtypes = L.ref_rad_authenticator_calc.argtypes
+    L.ref_rad_password_encode.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
+                                          ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    j = json.load(open(os.path.join(ROOT, "tests", "golden", "radius.json")))
+    secrets = [bytes.fromhex(s) for s in j["secrets"]]
+    L.ref_rad_sign.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.c_void_p, ctypes.POINTER(sz)]
+    out = ctypes.create_string_buffer(4096)
+    a16 = ctypes.create_string_buffer(16)
+    ol = sz()
+    for p in j["packets"]:
+        pre = bytes.fromhex(p["pre"])
+        assert L.ref_rad_sign(pre, len(pre), secrets[p["key"]], len(secrets[p["key"]]), out, ctypes.byref(ol)) == 0
+        assert out.raw[:ol.value].hex() == p["signed"]      # radius_pkt_sign on the drop-in md5.h
+        pkt = bytes.fromhex(p["signed"])
+        k = secrets[p["key"]]
+        req = bytes.fromhex(p["request"]) if p["kind"] == "reply" else None
+        assert L.ref_rad_verify(pkt, len(pkt), k, len(k), req, out) == 0
+        assert out.raw[:len(pkt)].hex() == p["verified"]
+        if p["kind"] == "reply":
+            assert L.ref_rad_authenticator_calc(pkt, len(pkt), k, len(k), 0, req, a16) == 0
+            assert a16.raw.hex() == p["authenticator_calc"]
+        if p["msg_authr"]:
+            assert L.ref_rad_msg_authenticator_calc(pkt, len(pkt), k, len(k), 0, req, a16) == 0
+    el = sz()
+    for v in j["password_encode"]:
+        pw, k = bytes.fromhex(v["password"]), secrets[v["key"]]
+        assert L.ref_rad_password_encode(bytes.fromhex(v["authenticator"]), pw, len(pw), k, len(k), out, 256,
+                                         ctypes.byref(el)) == 0
+        assert out.raw[:el.value].hex() == v["encoded"]

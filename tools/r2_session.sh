@@ -19,6 +19,7 @@ if [ -z "$SKIP_TESTS" ]; then
   step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS}
   rc=$?; [ $rc -ne 0 ] && exit $rc
 fi
+[ -n "$SKIP_BENCH" ] && exit 0
 step bench 400 python bench.py ${BENCH_ARGS} || exit $?
 step bench_c5 300 python bench.py --scaling strong --no-extras --no-cpu --steps 50 --warmup 20 || exit $?
 cd /tmp && export TMPDIR=/tmp
