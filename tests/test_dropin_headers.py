@@ -169,3 +169,25 @@ def test_reference_radius_sign_verify_with_dropin(tmp_path):
         assert L.ref_rad_password_encode(bytes.fromhex(v["authenticator"]), pw, len(pw), k, len(k), out, 256,
                                          ctypes.byref(el)) == 0
         assert out.raw[:el.value].hex() == v["encoded"]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference sources absent")
+def test_threadpool_queue_integration_compiles(tmp_path):
+    """INTEGRATION.md section 3 as a translation unit (tests/c/threadpool_queue.c):
+    a tp_task_pkt_rcvr_cb that submits to lcb_hash_queue and returns the
+    digest with tpt_msg_send compiles against the REFERENCE's thread-pool
+    headers; its only external references are liblcb's thread-pool calls
+    and this repo's queue ABI, which liblcb_hash_gpu.so exports."""
+    obj = str(tmp_path / "tpq.o")
+    subprocess.check_call(["gcc", "-c", "-O2", "-Wall", "-Werror", "-Wno-unused-function", "-Wno-unused-variable",
+                           "-I" + INC, "-I" + os.path.join(REF, "include")] + HAVE +
+                          ["-o", obj, os.path.join(C, "threadpool_queue.c")])
+    und = set(l.split()[-1] for l in subprocess.check_output(["nm", "-u", obj]).decode().splitlines())
+    ours = {"lcb_hash_queue_create", "lcb_hash_queue_settings_def", "lcb_hash_queue_submit"}
+    assert ours | {"tpt_get_current", "tpt_msg_send"} <= und
+    assert und - ours - {"tpt_get_current", "tpt_msg_send"} <= {"calloc", "free", "malloc", "memcpy",
+                                                                 "__stack_chk_fail"}
+    so = os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so")
+    if os.path.exists(so):
+        exported = subprocess.check_output(["nm", "-D", "--defined-only", so]).decode()
+        assert all((" T " + s) in exported for s in ours)
