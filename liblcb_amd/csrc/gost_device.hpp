@@ -147,7 +147,22 @@ __device__ __forceinline__ void gost_lps(uint64_t o[8], const uint64_t x[8], con
 
 // The flat table (one 16 KiB copy, entry (j, b) at T[j * 256 + b]): the
 // one-lane HMAC key-schedule prep kernel.
-struct GostFlat {
+// gost_g's hooks for tables whose LPS works on words in natural order: the
+// round constants are wave-uniform (scalar loads), N is added to word 0.
+struct GostNaturalOrder {
+    __device__ __forceinline__ static void to_lane(uint64_t o[8], const uint64_t v[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[i];
+    }
+    __device__ __forceinline__ static void from_lane(uint64_t o[8], const uint64_t v[8]) { to_lane(o, v); }
+    __device__ __forceinline__ static void xor_n(uint64_t x[8], uint64_t n0) { x[0] ^= n0; }
+    __device__ __forceinline__ static void xor_c(uint64_t x[8], const uint64_t k[8], int r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[r][i];
+    }
+};
+
+struct GostFlat : GostNaturalOrder {
     const uint64_t* T;
     __device__ __forceinline__ void lps(uint64_t o[8], const uint64_t x[8]) const { gost_lps(o, x, T); }
 };
@@ -169,7 +184,7 @@ struct GostFlat {
 using lds_u8 = __attribute__((address_space(3))) const uint8_t;
 using lds_u64 = __attribute__((address_space(3))) const uint64_t;
 
-struct GostRot {
+struct GostRot : GostNaturalOrder {
     lds_u8* L;
     uint32_t off[8];     // (8c + ((j' + r) & 7)) * 8
     uint32_t m1, m2, m4;  // all-ones where bit 0 / 1 / 2 of r is set
@@ -227,34 +242,38 @@ __device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
 
 // g_N(h, m) for a counter N whose upper 448 bits are zero (messages shorter
 // than 2^61 bytes; the ABI caps lengths at 2^32): gost3411-2012.h:1110-1144.
+// h and m in the table's lane order (natural order for GostFlat / GostRot;
+// the hooks let tools/gost_half.hpp's lane-ordered layout run the same code).
 template <class Tab>
 __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
     uint64_t k[8], t[8], x[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = h[i];
-    x[0] ^= n0;
+    T.xor_n(x, n0);
     T.lps(k, x);                                         // K = LPS(h ^ N)
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = k[i] ^ m[i];
     T.lps(t, x);                                         // t = LPS(K ^ m)
     // Rounds 1..11: K = LPS(K ^ C_{r-1}); t = LPS(t ^ K).  Kept rolled: the
-    // body is 128 LDS lookups already, the constants are wave-uniform loads.
+    // body is 128 LDS lookups already.  (Issuing t_r and K_{r+1} together --
+    // both need only K_r -- measured the same: tools/gost_lanes_ab.hip.)
 #pragma unroll 1
     for (int r = 0; r < 11; ++r) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[r][i];
+        T.xor_c(x, k, r);
         T.lps(k, x);                                     // K = LPS(K ^ C_r)
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = t[i] ^ k[i];
         T.lps(t, x);                                     // t = LPS(t ^ K)
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = k[i] ^ kGostC[11][i];
+    T.xor_c(x, k, 11);
     T.lps(k, x);                                         // K13 = LPS(K ^ C_11)
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] ^= m[i] ^ t[i] ^ k[i];  // :1142
 }
 
+// The chaining value h is kept in the table's lane order between blocks
+// (natural for the product's tables); Sigma and N in natural order.  The IV (all words equal) reads the
+// same in every order.
 template <bool k256>
 struct Gost {
     static constexpr int kBlock = 64, kDigest = k256 ? 32 : 64, kWords = 16;
@@ -267,12 +286,11 @@ struct Gost {
     // One g_N step over raw LE words w (gost3411-2012.h:1129-1131).
     template <class Tab>
     __device__ __forceinline__ void block(const uint32_t* w, uint64_t bits, const Tab& T) {
-        uint64_t m[8];
+        uint64_t m[8], ml[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
-        gost_g(h, n0, m, T);
-        n0 += bits;
-        // Sigma += m mod 2^512 (gost3411-2012.h:996-1013).
+        // Sigma += m mod 2^512 (gost3411-2012.h:996-1013), before g_N so
+        // that only the lane-ordered copy of m stays live through it.
         uint32_t carry = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -282,41 +300,55 @@ struct Gost {
             carry = c1 | (s2 < s1);
             sg[i] = s2;
         }
+        T.to_lane(ml, m);
+        gost_g(h, n0, ml, T);
+        n0 += bits;
     }
     // Tail + finalisation (gost3411-2012.h:1820-1839).
     template <class Tab>
     __device__ __forceinline__ void finish(uint32_t* w, uint32_t rem, const Tab& T) {
         put_byte(w, rem, 0x01u);
         block(w, (uint64_t)rem * 8u, T);
-        uint64_t m[8];
+        uint64_t m[8], ml[8];
         m[0] = n0;
 #pragma unroll
         for (int i = 1; i < 8; ++i) m[i] = 0;
-        gost_g(h, 0, m, T);   // g_0(h, N)
-        gost_g(h, 0, sg, T);  // g_0(h, Sigma)
+        T.to_lane(ml, m);
+        gost_g(h, 0, ml, T);   // g_0(h, N)
+        T.to_lane(ml, sg);
+        gost_g(h, 0, ml, T);   // g_0(h, Sigma)
     }
-    __device__ __forceinline__ void digest_words(uint32_t* out) const {
+    template <class Tab>
+    __device__ __forceinline__ void digest_words(uint32_t* out, const Tab& T) const {
         constexpr int first = 8 - kDigest / 8;  // last D bytes of h
+        uint64_t hn[8];
+        T.from_lane(hn, h);
 #pragma unroll
         for (int i = 0; i < kDigest / 8; ++i) {
-            out[2 * i] = (uint32_t)h[first + i];
-            out[2 * i + 1] = (uint32_t)(h[first + i] >> 32);
+            out[2 * i] = (uint32_t)hn[first + i];
+            out[2 * i + 1] = (uint32_t)(hn[first + i] >> 32);
         }
     }
-    __device__ __forceinline__ void save(uint32_t* p) const {
+    template <class Tab>
+    __device__ __forceinline__ void save(uint32_t* p, const Tab& T) const {
+        uint64_t hn[8];
+        T.from_lane(hn, h);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            p[2 * i] = (uint32_t)h[i]; p[2 * i + 1] = (uint32_t)(h[i] >> 32);
+            p[2 * i] = (uint32_t)hn[i]; p[2 * i + 1] = (uint32_t)(hn[i] >> 32);
             p[18 + 2 * i] = (uint32_t)sg[i]; p[19 + 2 * i] = (uint32_t)(sg[i] >> 32);
         }
         p[16] = (uint32_t)n0; p[17] = (uint32_t)(n0 >> 32);
     }
-    __device__ __forceinline__ void load(const uint32_t* p) {
+    template <class Tab>
+    __device__ __forceinline__ void load(const uint32_t* p, const Tab& T) {
+        uint64_t hn[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            h[i] = (uint64_t)p[2 * i] | ((uint64_t)p[2 * i + 1] << 32);
+            hn[i] = (uint64_t)p[2 * i] | ((uint64_t)p[2 * i + 1] << 32);
             sg[i] = (uint64_t)p[18 + 2 * i] | ((uint64_t)p[19 + 2 * i] << 32);
         }
+        T.to_lane(h, hn);
         n0 = (uint64_t)p[16] | ((uint64_t)p[17] << 32);
     }
 };

@@ -372,10 +372,13 @@ __global__ __launch_bounds__(64) void md_key_prep_kernel(KArgs a, uint32_t* mid)
 }
 
 // ------------------------------------------------------------------ GOST
-// Two waves per SIMD: the 64 KiB rotated LPS image (gost_device.hpp GostRot)
-// leaves room for two 256-thread workgroups per CU.
+// Four waves per SIMD: the 64 KiB rotated LPS image (gost_device.hpp GostRot)
+// leaves room for two 512-thread workgroups per CU, and the launch bound caps
+// the state at 128 VGPRs.  (Two 256-thread workgroups at up to 256 VGPRs:
+// 2-3 % slower; tools/gost_lanes_ab.hip)
+constexpr int kGostThreads = 512;
 template <bool k256, bool kHmac>
-__global__ __launch_bounds__(256, 2) void gost_batch_kernel(KArgs a) {
+__global__ __launch_bounds__(kGostThreads, 4) void gost_batch_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
     gost_stage_rot(Timg);
     GostRot T;
@@ -387,12 +390,12 @@ __global__ __launch_bounds__(256, 2) void gost_batch_kernel(KArgs a) {
     G st;
     uint32_t dw[G::kDigest / 4];
     if (kHmac) {
-        st.load(a.mid);
+        st.load(a.mid, T);
         gost_message(st, msg, len, T);
-        st.digest_words(dw);
+        st.digest_words(dw, T);
         // Outer pass: fresh state after K ^ opad, message = inner digest.
         G o;
-        o.load(a.mid + kMidWords);
+        o.load(a.mid + kMidWords, T);
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
@@ -404,18 +407,18 @@ __global__ __launch_bounds__(256, 2) void gost_batch_kernel(KArgs a) {
         } else {
             o.finish(w, G::kDigest, T);  // 32 bytes: the digest is the tail block
         }
-        o.digest_words(dw);
+        o.digest_words(dw, T);
     } else {
         st.init();
         gost_message(st, msg, len, T);
-        st.digest_words(dw);
+        st.digest_words(dw, T);
     }
     store_digest<G::kDigest>(a.digests + idx * G::kDigest, dw);
 }
 
 // Keyed GOST batches (see md_keyed_kernel).
 template <bool k256, int kMode>
-__global__ __launch_bounds__(256, 2) void gost_keyed_kernel(KArgs a) {
+__global__ __launch_bounds__(kGostThreads, 4) void gost_keyed_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];
     gost_stage_rot(Timg);
     GostRot T;
@@ -431,11 +434,11 @@ __global__ __launch_bounds__(256, 2) void gost_keyed_kernel(KArgs a) {
     G st;
     uint32_t dw[G::kDigest / 4];
     if (kMode == kKeyHmac) {
-        st.load(mid);
+        st.load(mid, T);
         gost_message(st, msg, len, T);
-        st.digest_words(dw);
+        st.digest_words(dw, T);
         G o;
-        o.load(mid + kMidWords);
+        o.load(mid + kMidWords, T);
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
@@ -447,16 +450,16 @@ __global__ __launch_bounds__(256, 2) void gost_keyed_kernel(KArgs a) {
         } else {
             o.finish(w, G::kDigest, T);
         }
-        o.digest_words(dw);
+        o.digest_words(dw, T);
     } else if (kMode == kKeyPrefix) {
         const uint64_t full = kl / 64 * 64;
-        st.load(mid);
+        st.load(mid, T);
         gost_message2(st, K + full, kl - full, msg, len, T);
-        st.digest_words(dw);
+        st.digest_words(dw, T);
     } else {
         st.init();
         gost_message2(st, msg, len, K, kl, T);
-        st.digest_words(dw);
+        st.digest_words(dw, T);
     }
     store_digest<G::kDigest>(a.digests + idx * G::kDigest, dw);
 }
@@ -466,7 +469,7 @@ template <bool k256>
 __global__ __launch_bounds__(256) void gost_key_prep_kernel(KArgs a, uint32_t* mid) {
     __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
     gost_stage_table(Timg);
-    const GostFlat T{Timg};
+    const GostFlat T{{}, Timg};
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.nkeys) return;
     using G = Gost<k256>;
@@ -481,13 +484,13 @@ __global__ __launch_bounds__(256) void gost_key_prep_kernel(KArgs a, uint32_t* m
             load_full64(K + 64 * b, w);
             st.block(w, 512, T);
         }
-        st.save(m);
+        st.save(m, T);
         return;
     }
     if (kl > 64) {  // gost3411-2012.h:1873-1878: long key -> its digest
         gost_message(st, K, kl, T);
         uint32_t dw[G::kDigest / 4];
-        st.digest_words(dw);
+        st.digest_words(dw, T);
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
     } else if (kl == 64) {
@@ -500,19 +503,19 @@ __global__ __launch_bounds__(256) void gost_key_prep_kernel(KArgs a, uint32_t* m
     for (int i = 0; i < 16; ++i) x[i] = w[i] ^ 0x36363636u;
     st.init();
     st.block(x, 512, T);
-    st.save(m);
+    st.save(m, T);
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = w[i] ^ 0x5c5c5c5cu;
     st.init();
     st.block(x, 512, T);
-    st.save(m + kMidWords);
+    st.save(m + kMidWords, T);
 }
 
 template <bool k256>
 __global__ void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid) {
     __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
     gost_stage_table(Timg);
-    const GostFlat T{Timg};
+    const GostFlat T{{}, Timg};
     if (threadIdx.x != 0) return;
     using G = Gost<k256>;
     uint32_t k[16];
@@ -523,7 +526,7 @@ __global__ void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t
         st.init();
         gost_message(st, dkey, key_len, T);
         uint32_t dw[G::kDigest / 4];
-        st.digest_words(dw);
+        st.digest_words(dw, T);
 #pragma unroll
         for (int i = 0; i < 16; ++i) k[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
     }
@@ -533,12 +536,12 @@ __global__ void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t
     for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x36363636u;
     st.init();
     st.block(w, 512, T);
-    st.save(mid);
+    st.save(mid, T);
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x5c5c5c5cu;
     st.init();
     st.block(w, 512, T);
-    st.save(mid + kMidWords);
+    st.save(mid + kMidWords, T);
 }
 
 // ------------------------------------------------------ synthetic input
@@ -679,8 +682,9 @@ static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
 }
 template <bool k256>
 static void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
-    if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), grid_for(a.count), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), grid_for(a.count), dim3(256), 0, s, a);
+    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
+    if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), g, dim3(kGostThreads), 0, s, a);
+    else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), g, dim3(kGostThreads), 0, s, a);
 }
 
 template <class H>
@@ -693,10 +697,11 @@ static void launch_md_keyed(const KArgs& a, hipStream_t s) {
 }
 template <bool k256>
 static void launch_gost_keyed(const KArgs& a, hipStream_t s) {
+    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
     switch (a.key_mode) {
-    case kKeyHmac: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyHmac>), grid_for(a.count), dim3(256), 0, s, a); break;
-    case kKeyPrefix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyPrefix>), grid_for(a.count), dim3(256), 0, s, a); break;
-    case kKeySuffix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeySuffix>), grid_for(a.count), dim3(256), 0, s, a); break;
+    case kKeyHmac: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyHmac>), g, dim3(kGostThreads), 0, s, a); break;
+    case kKeyPrefix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyPrefix>), g, dim3(kGostThreads), 0, s, a); break;
+    case kKeySuffix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeySuffix>), g, dim3(kGostThreads), 0, s, a); break;
     }
 }
 
