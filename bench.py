@@ -460,25 +460,35 @@ def bench_chacha(data, count, steps):
 def bench_ingest(alg_id, packets=1 << 21, threads=8):
     """Asynchronous ingestion queue (include/lcb_hash_queue.h, SURVEY.md 8f
     row 2): `threads` native producer threads submit 1 KiB packets from host
-    memory; packets/s and submit->callback latency, plus the same producers
-    doing only the memcpy into host memory (the host-side ceiling).  Runs
-    tools/queue_bench as a child process."""
+    memory.  Three runs of tools/queue_bench (a child process): saturation
+    (producers as fast as they can: packets/s; its latency is queueing behind
+    an overload by construction), open loop at half that rate (packets due
+    on a fixed schedule, latency counted from the due time: the latency a
+    caller below capacity sees), and the producers' memcpy alone (the
+    host-side ceiling)."""
     exe = os.path.join(ROOT, "tools", "queue_bench")
     if not os.path.exists(exe):
         return {"skipped": "tools/queue_bench not built"}
     base = [exe, "--alg", str(alg_id), "--packets", str(packets), "--size", str(MSG_LEN),
             "--threads", str(threads)]
-    res = {}
-    for key, extra in (("queue", []), ("copy_only", ["--copy-only", "1"])):
+
+    def run(extra):
         r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
-            return {"error": r.stderr.strip()[-300:]}
-        res[key] = json.loads(r.stdout.strip().splitlines()[-1])
-    q = res["queue"]
-    return {"packets_per_s": q["packets_per_s"], "GiB_s": q["GiB_s"], "lat_us_p50": q["lat_us_p50"],
-            "lat_us_p99": q["lat_us_p99"], "batches": q["batches"], "threads": threads,
-            "packet_bytes": MSG_LEN, "settings": "64K packets / 64 MiB / 200 us / 4 slots",
-            "copy_only_GiB_s": res["copy_only"]["GiB_s"],
+            raise RuntimeError(r.stderr.strip()[-300:])
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    try:
+        sat = run([])
+        half = run(["--rate", str(int(sat["packets_per_s"] / 2))])
+        copy = run(["--copy-only", "1"])
+    except RuntimeError as e:
+        return {"error": str(e)}
+    return {"packets_per_s": sat["packets_per_s"], "GiB_s": sat["GiB_s"], "batches": sat["batches"],
+            "saturated_lat_us_p50": sat["lat_us_p50"], "saturated_lat_us_p99": sat["lat_us_p99"],
+            "half_load_packets_per_s": half["packets_per_s"], "half_load_lat_us_p50": half["lat_us_p50"],
+            "half_load_lat_us_p99": half["lat_us_p99"], "half_load_lat_us_p999": half["lat_us_p999"],
+            "half_load_lat_us_max": half["lat_us_max"], "threads": threads, "packet_bytes": MSG_LEN,
+            "settings": "64K packets / 64 MiB / 200 us / 4 slots", "copy_only_GiB_s": copy["GiB_s"],
             "path": "producer memcpy into pinned lease -> H2D -> kernel -> D2H -> per-packet callback"}
 
 

@@ -19,6 +19,9 @@
  *   - a flusher thread seals the open batch when it is full
  *     (max_batch_msgs / max_batch_bytes) or its first packet is flush_usec
  *     old, DMAs it to HBM, runs the batch kernel and copies the digests back;
+ *     while every other staging slot is still in flight an old batch stays
+ *     open (it could not start sooner) and is sealed as soon as a slot is
+ *     returned, so batches grow with the load instead of producers blocking;
  *   - a completion thread delivers every digest: it is copied to the
  *     submitter's `digest` pointer (if any) and `cb(udata, error, digest,
  *     size)` is called (if any).  The callback runs on the queue's
@@ -78,6 +81,12 @@ typedef struct lcb_hash_queue_stats_s {
 	uint64_t	flusher_launch_ns; /* Flusher: enqueueing copies and kernels. */
 	uint64_t	completer_busy_ns; /* Completer: digest copies + callbacks. */
 	uint64_t	gpu_wait_ns;	/* Completer: waiting for launched batches. */
+	/* Worst single batch / submit seen, per pipeline stage (ns): */
+	uint64_t	max_fill_ns;	/* first packet in a slot -> its seal. */
+	uint64_t	max_launch_ns;	/* seal -> copies and kernel enqueued. */
+	uint64_t	max_gpu_ns;	/* enqueued (or the completer free) -> done. */
+	uint64_t	max_callback_ns; /* a batch's digest copies + callbacks. */
+	uint64_t	max_submit_wait_ns; /* a submit blocked for an open slot. */
 } lcb_hash_queue_stats_t;
 
 /* Submit flags. */

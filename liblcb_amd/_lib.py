@@ -94,7 +94,8 @@ class QueueStats(ctypes.Structure):
     _fields_ = [(n, c_u64) for n in ("packets", "bytes", "batches", "sealed_full", "sealed_timer",
                                      "sealed_flush", "max_batch_msgs", "submit_waits",
                                      "flusher_drain_ns", "flusher_launch_ns", "completer_busy_ns",
-                                     "gpu_wait_ns")]
+                                     "gpu_wait_ns", "max_fill_ns", "max_launch_ns", "max_gpu_ns",
+                                     "max_callback_ns", "max_submit_wait_ns")]
 
 
 class Seg(ctypes.Structure):

@@ -73,18 +73,18 @@ int cha_enqueue(ChaArgs a, bool x, hipStream_t s) {
     uint32_t* subkeys = nullptr;
     const uint64_t nparts = (a.count + 1023) / 1024;
     if (a.lengths)
-        CHA_TRY(hipMallocAsync(reinterpret_cast<void**>(&scan), (nparts + a.count + 1) * 8, s));
+        CHA_TRY(scratch_alloc(reinterpret_cast<void**>(&scan), (nparts + a.count + 1) * 8, s));
     if (x) {
-        hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&subkeys), a.count * 32, s);
+        hipError_t e = scratch_alloc(reinterpret_cast<void**>(&subkeys), a.count * 32, s);
         if (e != hipSuccess) {
-            if (scan) (void)hipFreeAsync(scan, s);
+            if (scan) (void)scratch_free(scan, s);
             return map_err(e);
         }
     }
     launch_chacha(a, nparts, scan, scan ? scan + nparts : nullptr, subkeys, s);
     hipError_t e = hipGetLastError();
-    if (scan) (void)hipFreeAsync(scan, s);
-    if (subkeys) (void)hipFreeAsync(subkeys, s);
+    if (scan) (void)scratch_free(scan, s);
+    if (subkeys) (void)scratch_free(subkeys, s);
     return map_err(e);
 }
 

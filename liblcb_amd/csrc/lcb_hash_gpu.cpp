@@ -51,9 +51,47 @@ int map_err(hipError_t e) {
         if (_e != hipSuccess) return map_err(_e); \
     } while (0)
 
+// ------------------------------------------------------------ scratch pool
+namespace {
+std::mutex g_scratch_mu;
+hipMemPool_t g_scratch[64];
+}  // namespace
+
+static hipMemPool_t scratch_pool(int dev) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (g_scratch[dev]) return g_scratch[dev];
+    hipMemPoolProps props;
+    memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) return nullptr;
+    int off = 0;
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseFollowEventDependencies, &off);
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowOpportunistic, &off);
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowInternalDependencies, &off);
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    g_scratch[dev] = pool;
+    return pool;
+}
+
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    hipMemPool_t pool = scratch_pool(dev);
+    if (!pool) return hipErrorOutOfMemory;
+    return hipMallocFromPoolAsync(p, bytes, pool, s);
+}
+
+hipError_t scratch_free(void* p, hipStream_t s) { return hipFreeAsync(p, s); }
+
 // HMAC: build the key block / long-key buffer and enqueue the mid-state prep
-// kernel.  *mid receives a stream-ordered allocation the caller frees with
-// hipFreeAsync after the batch kernel.
+// kernel.  *mid receives a scratch allocation the caller frees with
+// scratch_free after the batch kernel.
 int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
                uint8_t** dkey_out) {
     KeyBlock kb;
@@ -65,11 +103,11 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
     } else {
         // Long key: hashed on the device.  The copy is waited for so the
         // caller may release `key` on return (pageable source memory).
-        LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&dkey), key_len, s));
+        LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dkey), key_len, s));
         LCB_TRY(hipMemcpyAsync(dkey, key, key_len, hipMemcpyHostToDevice, s));
         LCB_TRY(hipStreamSynchronize(s));
     }
-    LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(mid), 2 * kMidWords * sizeof(uint32_t), s));
+    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(mid), 2 * kMidWords * sizeof(uint32_t), s));
     launch_hmac_prep(alg, kb, dkey, key_len, *mid, s);
     LCB_TRY(hipGetLastError());
     *dkey_out = dkey;
@@ -78,21 +116,25 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
 
 // Launch the batch kernel, bucketing a large ragged batch by length first
 // (stream-ordered temporaries, no synchronisation).
-int launch_ordered(int alg, KArgs a, hipStream_t s) {
+int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     uint32_t* work = nullptr;
     // The bucketing permutation holds message indices as uint32.
     if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
         // work: [kLenClasses class cursors | 1 tile-queue head | count order]
         const size_t bytes = (kLenClasses + 1 + a.count) * sizeof(uint32_t);
-        LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&work), bytes, s));
+        if (work_buf) {
+            work = work_buf;
+        } else {
+            LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&work), bytes, s));
+        }
         launch_bucketing(a.lengths, a.count, work, work + kLenClasses + 1, s);
         a.tile_next = work + kLenClasses;
         a.order = work + kLenClasses + 1;
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();
-    if (work) (void)hipFreeAsync(work, s);
+    if (work && work != work_buf) (void)scratch_free(work, s);
     return map_err(e);
 }
 
@@ -178,8 +220,8 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
         a.mid = mid;
     }
     int rc = launch_ordered(alg, a, s);
-    if (mid) (void)hipFreeAsync(mid, s);
-    if (dkey) (void)hipFreeAsync(dkey, s);
+    if (mid) (void)scratch_free(mid, s);
+    if (dkey) (void)scratch_free(dkey, s);
     return rc;
 }
 
@@ -414,8 +456,8 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     int rc2 = drain(0);
     int rc3 = drain(1);
     if (mid || dkey) {  // both streams are drained: release the HMAC state
-        if (mid) (void)hipFreeAsync(mid, S.st[0]);
-        if (dkey) (void)hipFreeAsync(dkey, S.st[0]);
+        if (mid) (void)scratch_free(mid, S.st[0]);
+        if (dkey) (void)scratch_free(dkey, S.st[0]);
         (void)hipStreamSynchronize(S.st[0]);
     }
     if (rc) return rc;
@@ -503,7 +545,7 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = nkeys * 4;
     const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
     uint8_t* dbuf = nullptr;
-    LCB_TRY(hipMallocAsync(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b, s));
+    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b, s));
     KeyTable kt;
     kt.mode = (uint32_t)key_mode;
     kt.keys = dbuf;
@@ -531,7 +573,7 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
                       : batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
                                    nullptr, nullptr, &kt);
     }
-    (void)hipFreeAsync(dbuf, s);
+    (void)scratch_free(dbuf, s);
     if (!dev_mode) (void)hipStreamSynchronize(s);
     return rc;
 }

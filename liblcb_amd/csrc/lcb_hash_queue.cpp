@@ -84,6 +84,7 @@ struct Slot {
     alignas(64) std::atomic<uint32_t> gen{0};    // bumped each time the slot reopens
     std::atomic<uint32_t> closed{0};             // read-mostly copy of the seal for lease holders
     std::atomic<int64_t> t_first{0};             // ns timestamp of the first packet; 0 = none
+    int64_t t_seal = 0, t_launch = 0;            // flusher: sealed / enqueued (ns)
     uint64_t seq = 0;                            // open order (wait() bookkeeping)
     uint8_t* h_data = nullptr;
     uint64_t* h_off = nullptr;
@@ -96,6 +97,7 @@ struct Slot {
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
     uint8_t* d_dig = nullptr;
+    uint32_t* d_work = nullptr;                  // bucketing scratch (launch_ordered)
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     size_t n = 0, bytes = 0, payload = 0, packets = 0;  // final shape of a sealed batch
@@ -127,6 +129,12 @@ inline void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
+void note_max(std::atomic<uint64_t>& m, int64_t v) {
+    if (v <= 0) return;
+    uint64_t cur = m.load(std::memory_order_relaxed);
+    while ((uint64_t)v > cur && !m.compare_exchange_weak(cur, (uint64_t)v, std::memory_order_relaxed)) {}
 }
 
 // A producer thread's current lease in one queue.
@@ -174,6 +182,7 @@ struct lcb_hash_queue_s {
     std::atomic<uint64_t> batches{0}, sealed_full{0}, sealed_timer{0}, sealed_flush{0};
     std::atomic<uint64_t> max_batch{0}, submit_waits{0};
     std::atomic<uint64_t> drain_ns{0}, launch_ns{0}, completer_ns{0}, gpu_wait_ns{0};
+    std::atomic<uint64_t> max_fill{0}, max_launch{0}, max_gpu{0}, max_cb{0}, max_submit_wait{0};
     std::atomic<int> first_error{0};
 
     std::thread flusher, completer;
@@ -256,11 +265,12 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
         hipMemcpyAsync(b->d_len, b->h_len, b->n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
         (b->bytes && hipMemcpyAsync(b->d_data, b->h_data, b->bytes, hipMemcpyHostToDevice, st) != hipSuccess))
         rc = EIO;
-    if (!rc) rc = launch_ordered(alg, a, st);
+    if (!rc) rc = launch_ordered(alg, a, st, b->d_work);
     if (!rc && hipMemcpyAsync(b->h_dig, b->d_dig, b->n * D, hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = EIO;
     if (!rc && hipEventRecord(b->done, st) != hipSuccess) rc = EIO;
     b->launch_err = rc;
+    b->t_launch = now_ns();
     batches.fetch_add(1, std::memory_order_relaxed);
     uint64_t mb = max_batch.load(std::memory_order_relaxed);
     while (b->n > mb && !max_batch.compare_exchange_weak(mb, b->n)) {}
@@ -296,7 +306,17 @@ void lcb_hash_queue_s::flusher_main() {
                 if (st_count(s) == 0) flush_req.store(false, std::memory_order_release);
                 if (t0 != 0) {
                     const auto due = Clock::time_point(std::chrono::nanoseconds(t0)) + window;
-                    if (Clock::now() >= due) { why = kSealTimer; break; }
+                    if (Clock::now() >= due) {
+                        // The window is over; seal only when a free slot can
+                        // take over at once.  With every other slot still on
+                        // the GPU the batch could not start earlier anyway:
+                        // it keeps filling (larger batches under load, no
+                        // producer blocked) until a slot is returned (the
+                        // completer notifies), it is full, or a flush.
+                        if (!free_slots.empty()) { why = kSealTimer; break; }
+                        cv_flusher.wait_for(lk, std::chrono::milliseconds(50));
+                        continue;
+                    }
                     cv_flusher.wait_until(lk, due);
                 } else {
                     cv_flusher.wait_for(lk, std::chrono::milliseconds(50));
@@ -304,23 +324,43 @@ void lcb_hash_queue_s::flusher_main() {
             }
         }
         seal(b);  // no-op when a producer already sealed it as full
+        b->t_seal = now_ns();
+        note_max(max_fill, b->t_seal - b->t_first.load(std::memory_order_relaxed));
         flush_req.store(false, std::memory_order_release);
-        // Reopen first (producers only ever wait for a free slot, never for
-        // the launch below), then drain and launch the sealed slot.
+        // Reopen at once when a slot is free (producers then wait only for the
+        // install, never for the launch below).  When every other slot is still
+        // in flight, launch the sealed slot FIRST: waiting for a free slot
+        // before its launch would hold the batch back for a whole GPU round.
+        bool reopened = false;
         {
             std::unique_lock<std::mutex> lk(m);
-            cv_free.wait(lk, [&] { return !free_slots.empty(); });
-            Slot* next = free_slots.front();
-            free_slots.pop_front();
-            install_open(next);
+            if (!free_slots.empty()) {
+                Slot* next = free_slots.front();
+                free_slots.pop_front();
+                install_open(next);
+                reopened = true;
+            }
         }
-        cv_open.notify_all();
+        if (reopened) cv_open.notify_all();
         const int64_t t_busy = now_ns();
         drain_leases(b);
         const int64_t t_launch = now_ns();
-        launch(b, why);
+        const int64_t t_seal = b->t_seal;
+        launch(b, why);   // b may complete and be reused from here on: no access
+        const int64_t t_end = now_ns();
+        note_max(max_launch, t_end - t_seal);
         drain_ns.fetch_add(t_launch - t_busy, std::memory_order_relaxed);
-        launch_ns.fetch_add(now_ns() - t_launch, std::memory_order_relaxed);
+        launch_ns.fetch_add(t_end - t_launch, std::memory_order_relaxed);
+        if (!reopened) {
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv_free.wait(lk, [&] { return !free_slots.empty(); });
+                Slot* next = free_slots.front();
+                free_slots.pop_front();
+                install_open(next);
+            }
+            cv_open.notify_all();
+        }
     }
 }
 
@@ -339,6 +379,7 @@ void lcb_hash_queue_s::completer_main() {
         if (!err) err = map_err(hipEventSynchronize(b->done));
         const int64_t t_cb = now_ns();
         gpu_wait_ns.fetch_add(t_cb - t_wait, std::memory_order_relaxed);
+        note_max(max_gpu, t_cb - std::max(t_wait, b->t_launch));
         for (size_t i = 0; i < b->n; ++i) {
             const Meta& mt = b->meta[i];
             if (!mt.real) continue;
@@ -350,7 +391,9 @@ void lcb_hash_queue_s::completer_main() {
             int z = 0;
             first_error.compare_exchange_strong(z, err);
         }
-        completer_ns.fetch_add(now_ns() - t_cb, std::memory_order_relaxed);
+        const int64_t t_end = now_ns();
+        completer_ns.fetch_add(t_end - t_cb, std::memory_order_relaxed);
+        note_max(max_cb, t_end - t_cb);
         completed.fetch_add(b->packets, std::memory_order_relaxed);
         completed_bytes.fetch_add(b->payload, std::memory_order_relaxed);
         {
@@ -360,6 +403,7 @@ void lcb_hash_queue_s::completer_main() {
             free_slots.push_back(b);
         }
         cv_free.notify_one();
+        cv_flusher.notify_one();   // a batch held open for want of a slot may go now
         cv_done.notify_all();
     }
 }
@@ -387,6 +431,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_off), msgs * 8));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_len), msgs * 4));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_dig), msgs * D));
+    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), (kLenClasses + 1 + msgs) * sizeof(uint32_t)));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
     b.leases = new (std::nothrow) LeaseRec[nleases];
@@ -403,12 +448,13 @@ void free_slot(Slot& b) {
     if (b.d_off) (void)hipFree(b.d_off);
     if (b.d_len) (void)hipFree(b.d_len);
     if (b.d_dig) (void)hipFree(b.d_dig);
+    if (b.d_work) (void)hipFree(b.d_work);
     if (b.done) (void)hipEventDestroy(b.done);
     if (b.stream) (void)hipStreamDestroy(b.stream);
     delete[] b.meta;
     delete[] b.leases;
     b.h_data = nullptr; b.h_off = nullptr; b.h_len = nullptr; b.h_dig = nullptr; b.meta = nullptr;
-    b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_dig = nullptr;
+    b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_dig = nullptr; b.d_work = nullptr;
     b.done = nullptr; b.stream = nullptr; b.leases = nullptr; b.nleases = 0;
 }
 
@@ -483,8 +529,8 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
                 hipMemcpyAsync(keep, mid, 2 * kMidWords * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) !=
                     hipSuccess)
                 rc = ENOMEM;
-            (void)hipFreeAsync(mid, st);
-            if (dkey) (void)hipFreeAsync(dkey, st);
+            (void)scratch_free(mid, st);
+            if (dkey) (void)scratch_free(dkey, st);
             if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = EIO;
             q->mid = keep;
         }
@@ -593,12 +639,22 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
             L.valid = true;
             continue;
         }
-        // Sealed: wait until the flusher installs a new open slot.
+        // Sealed: wait until the flusher installs a new open slot.  The
+        // install normally follows the seal within a microsecond or two: spin
+        // that long before sleeping on the condition variable (a futex
+        // wake-up costs tens of microseconds).
+        if (flags & LCB_HASH_Q_F_NOWAIT) {
+            if (q->open.load(std::memory_order_acquire) == b) return EAGAIN;
+            continue;
+        }
+        const int64_t t_w = now_ns();
+        for (int k = 0; k < 2000 && q->open.load(std::memory_order_acquire) == b; ++k) _mm_pause();
+        if (q->open.load(std::memory_order_acquire) != b) continue;
         std::unique_lock<std::mutex> lk(q->m);
         if (q->open.load(std::memory_order_acquire) == b) {
-            if (flags & LCB_HASH_Q_F_NOWAIT) return EAGAIN;
             if (!waited) { q->submit_waits.fetch_add(1, std::memory_order_relaxed); waited = true; }
             q->cv_open.wait(lk, [&] { return q->open.load(std::memory_order_acquire) != b; });
+            note_max(q->max_submit_wait, now_ns() - t_w);
         }
     }
 }
@@ -650,6 +706,11 @@ int lcb_hash_queue_stats(lcb_hash_queue_p q, lcb_hash_queue_stats_t* st) {
     st->flusher_launch_ns = q->launch_ns.load();
     st->completer_busy_ns = q->completer_ns.load();
     st->gpu_wait_ns = q->gpu_wait_ns.load();
+    st->max_fill_ns = q->max_fill.load();
+    st->max_launch_ns = q->max_launch.load();
+    st->max_gpu_ns = q->max_gpu.load();
+    st->max_callback_ns = q->max_cb.load();
+    st->max_submit_wait_ns = q->max_submit_wait.load();
     return 0;
 }
 

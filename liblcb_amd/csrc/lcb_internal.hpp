@@ -105,12 +105,21 @@ size_t bsize(int alg);                  // block bytes (HMAC key block)
 int map_err(hipError_t e);              // HIP error -> liblcb errno code
 int ensure_init();                      // 0, or ENODEV without a usable device
 int device_cu_count();                  // compute units of the current device (cached)
-// Enqueue the HMAC mid-state prep; *mid / *dkey are stream-ordered
-// allocations the caller releases with hipFreeAsync after its last use.
+// Stream-ordered scratch from the library's own pool on the current device
+// (one per device).  The pool reuses freed memory only on the stream that
+// freed it: the default pool's cross-stream reuse handed one live
+// bucketing buffer to two batches running concurrently on different streams
+// (the ingestion queue's slots).  Memory stays in the pool.
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
+hipError_t scratch_free(void* p, hipStream_t s);
+// Enqueue the HMAC mid-state prep; *mid / *dkey are scratch allocations
+// the caller releases with scratch_free after their last use.
 int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
                uint8_t** dkey_out);
 // Batch kernel launch, bucketing a large ragged batch by length first.
-int launch_ordered(int alg, KArgs a, hipStream_t s);
+// work_buf: optional caller-owned device buffer of (kLenClasses + 1 + count)
+// uint32 for the bucketing of a ragged batch; null = stream-ordered allocation.
+int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf = nullptr);
 
 // The two batch paths of lcb_hash_batch (lcb_hash_gpu.cpp), on the current
 // device.  batch_device enqueues on `s`; batch_host stages through `stage`

@@ -209,6 +209,58 @@ def test_native_producers(gpu, oracle, tmp_path, alg, key):
 
 
 @pytest.mark.gpu
+def test_native_producers_repeated(gpu, oracle, tmp_path):
+    """Regression: 4 slots of 4096-packet batches run concurrently on four
+    streams, each bucketed through its own scratch.  With the default
+    stream-ordered pool a live bucketing buffer could be handed to a second
+    batch on another stream, and 1-3 runs in 20 delivered whole batches of
+    another packet's digests; six runs in a row must all be exact."""
+    import json
+    import os
+    import subprocess
+    from oracle.pyoracle import SEED, gen_stream
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "queue_bench")
+    n, size = 1 << 16, 1024
+    want = oracle.batch_fixed_mt(MD5, gen_stream(SEED, n * size), n, size, size)
+    out = tmp_path / "dig.bin"
+    for it in range(6):
+        r = subprocess.run([exe, "--alg", str(MD5), "--packets", str(n), "--size", str(size), "--threads", "8",
+                            "--batch-msgs", "4096", "--out", str(out)], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        got = np.fromfile(out, np.uint8).reshape(n, 16)
+        bad = np.nonzero((got != want).any(1))[0]
+        assert len(bad) == 0, (it, len(bad), bad[:8])
+
+
+@pytest.mark.gpu
+def test_concurrent_ragged_batches_on_streams(gpu, oracle):
+    """Device-mode ragged batches (bucketed: >= 4096 messages) launched on four
+    streams at once, repeatedly: each batch's scratch stays its own."""
+    import torch
+    rng = np.random.default_rng(77)
+    jobs = []
+    for k in range(4):
+        n = 6000 + 1000 * k
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        from oracle.pyoracle import gen_stream
+        data = gen_stream(100 + k, int(lens.sum()) + 8)
+        jobs.append((data, offs, lens, oracle.batch(MD5, data, offs, lens)))
+    dev = [(torch.as_tensor(d, device="cuda"), torch.as_tensor(o.astype(np.int64), device="cuda"),
+            torch.as_tensor(l.astype(np.int32), device="cuda")) for d, o, l, _ in jobs]
+    streams = [torch.cuda.Stream() for _ in jobs]
+    for rep in range(10):
+        outs = []
+        for (dd, do, dl), st in zip(dev, streams):
+            with torch.cuda.stream(st):
+                outs.append(gpu.hash_batch(MD5, dd, offsets=do, lengths=dl))
+        torch.cuda.synchronize()
+        for (_, _, _, exp), got in zip(jobs, outs):
+            assert np.array_equal(got.cpu().numpy(), exp), rep
+
+
+@pytest.mark.gpu
 def test_stale_lease_across_generations(gpu, oracle):
     """One producer goes idle holding a lease while the others cycle the slots
     through many generations (2 slots, 16-message batches); when it wakes its

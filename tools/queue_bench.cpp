@@ -13,6 +13,14 @@
 // usage: queue_bench [--alg 1] [--packets 1048576] [--size 1024] [--threads 8]
 //                    [--flush-us 200] [--batch-msgs 65536] [--batch-bytes 67108864]
 //                    [--slots 4] [--align 16] [--key HEX] [--cb 1] [--pool-mib 0] [--out FILE]
+//                    [--rate PACKETS_PER_S]
+//
+// --rate: open loop.  Producer t's k-th packet is due at t0 + (k * threads + t)
+// / rate (an aggregate rate of `rate`); a producer spins until it is due and the
+// latency is counted from the DUE time, so a producer running late (the
+// queue pushing back) adds its lateness to the latency instead of hiding it.
+// Without --rate the producers submit as fast as they can (saturation: the
+// latency then includes the time blocked waiting for a free slot).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,6 +32,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <emmintrin.h>
 
 #include "../include/lcb_hash_gpu.h"
 #include "../include/lcb_hash_queue.h"
@@ -65,6 +75,7 @@ int main(int argc, char** argv) {
     bool use_cb = true;
     bool copy_only = false;  // baseline: producers only memcpy into a private arena
     uint64_t pool_mib = 0;  // 0: every packet distinct (cold source); else cycle a pool this big
+    double rate = 0;        // packets/s offered (open loop); 0: as fast as possible
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i], v = argv[i + 1];
         if (a == "--alg") alg = atoi(v.c_str());
@@ -81,6 +92,7 @@ int main(int argc, char** argv) {
         else if (a == "--cb") use_cb = atoi(v.c_str()) != 0;
         else if (a == "--pool-mib") pool_mib = strtoull(v.c_str(), nullptr, 0);
         else if (a == "--copy-only") copy_only = atoi(v.c_str()) != 0;
+        else if (a == "--rate") rate = atof(v.c_str());
         else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
     const size_t D = lcb_hash_digest_size(alg);
@@ -152,6 +164,21 @@ int main(int argc, char** argv) {
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t)
             th.emplace_back([&, t] {
+                if (rate > 0) {
+                    // contiguous packets per producer (as without --rate); the
+                    // k-th packet of producer t is due at (k * threads + t) / rate
+                    const double gap = 1e9 / rate;
+                    const uint64_t lo = packets * t / threads, hi = packets * (t + 1) / threads;
+                    for (uint64_t i = lo; i < hi; ++i) {
+                        const int64_t due = t0 + (int64_t)(((i - lo) * threads + t) * gap);
+                        while (now_ns() < due) _mm_pause();
+                        t_sub[i] = due;
+                        int r = lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &digests[i * D],
+                                                      use_cb ? on_done : nullptr, (void*)(uintptr_t)i, 0);
+                        if (r) { fail.store(r); return; }
+                    }
+                    return;
+                }
                 const uint64_t lo = packets * t / threads, hi = packets * (t + 1) / threads;
                 for (uint64_t i = lo; i < hi; ++i) {
                     t_sub[i] = now_ns();
@@ -174,15 +201,23 @@ int main(int argc, char** argv) {
     }
     std::vector<double> lat(packets);
     for (uint64_t i = 0; i < packets; ++i) lat[i] = use_cb ? (t_done[i] - t_sub[i]) * 1e-3 : 0.0;
+    // the second half of the run alone (start-up effects excluded)
+    std::vector<double> lat2(lat.begin() + packets / 2, lat.end());
+    std::sort(lat2.begin(), lat2.end());
+    // where the worst packet sits in the run (fraction of the submit order)
+    const uint64_t worst = std::max_element(lat.begin(), lat.end()) - lat.begin();
     std::sort(lat.begin(), lat.end());
     const double sec = (t1 - t0) * 1e-9;
-    printf("{\"alg\": %d, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"flush_usec\": %u, "
+    printf("{\"alg\": %d, \"rate\": %.0f, \"lat_us_p999\": %.1f, \"late_half_p99\": %.1f, \"late_half_max\": %.1f, "
+           "\"worst_at\": %.4f, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"flush_usec\": %u, "
            "\"batch_msgs\": %llu, \"batch_bytes\": %llu, \"slots\": %u, \"pool_mib\": %llu, \"seconds\": %.4f, "
            "\"packets_per_s\": %.0f, \"GiB_s\": %.3f, \"lat_us_p50\": %.1f, \"lat_us_p99\": %.1f, "
            "\"lat_us_max\": %.1f, \"batches\": %llu, \"sealed_full\": %llu, \"sealed_timer\": %llu, "
            "\"sealed_flush\": %llu, \"submit_waits\": %llu, \"cb\": %d, \"drain_ms\": %.2f, \"launch_ms\": %.2f, "
-           "\"completer_busy_ms\": %.2f, \"gpu_wait_ms\": %.2f}\n",
-           alg, (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
+           "\"completer_busy_ms\": %.2f, \"gpu_wait_ms\": %.2f, \"max_fill_us\": %.1f, \"max_launch_us\": %.1f, "
+           "\"max_gpu_us\": %.1f, \"max_callback_us\": %.1f, \"max_submit_wait_us\": %.1f}\n",
+           alg, rate, lat[packets * 999 / 1000], lat2[lat2.size() * 99 / 100], lat2.back(), (double)worst / packets,
+           (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
            (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, (unsigned long long)pool_mib, sec,
            packets / sec, nbytes / sec / (1ull << 30), lat[packets / 2], lat[packets * 99 / 100],
            lat[packets - 1], (unsigned long long)(st.batches - st0.batches),
@@ -191,7 +226,8 @@ int main(int argc, char** argv) {
            (unsigned long long)(st.sealed_flush - st0.sealed_flush),
            (unsigned long long)(st.submit_waits - st0.submit_waits), (int)use_cb,
            (st.flusher_drain_ns - st0.flusher_drain_ns) * 1e-6, (st.flusher_launch_ns - st0.flusher_launch_ns) * 1e-6, (st.completer_busy_ns - st0.completer_busy_ns) * 1e-6,
-           (st.gpu_wait_ns - st0.gpu_wait_ns) * 1e-6);
+           (st.gpu_wait_ns - st0.gpu_wait_ns) * 1e-6, st.max_fill_ns * 1e-3, st.max_launch_ns * 1e-3,
+           st.max_gpu_ns * 1e-3, st.max_callback_ns * 1e-3, st.max_submit_wait_ns * 1e-3);
     if (!out.empty()) {
         FILE* f = fopen(out.c_str(), "wb");
         if (!f || fwrite(digests.data(), 1, digests.size(), f) != digests.size()) return 1;
