@@ -18,10 +18,9 @@
  *     the call returns;
  *   - a flusher thread seals the open batch when it is full
  *     (max_batch_msgs / max_batch_bytes) or its first packet is flush_usec
- *     old, DMAs it to HBM, runs the batch kernel and copies the digests back;
- *     while every other staging slot is still in flight an old batch stays
- *     open (it could not start sooner) and is sealed as soon as a slot is
- *     returned, so batches grow with the load instead of producers blocking;
+ *     old, DMAs it to HBM, runs the batch kernel and copies the digests back
+ *     (with every staging slot in flight, the sealed batch is launched first
+ *     and producers wait for the next slot to be returned);
  *   - a completion thread delivers every digest: it is copied to the
  *     submitter's `digest` pointer (if any) and `cb(udata, error, digest,
  *     size)` is called (if any).  The callback runs on the queue's

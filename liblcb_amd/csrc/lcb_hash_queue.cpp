@@ -307,15 +307,8 @@ void lcb_hash_queue_s::flusher_main() {
                 if (t0 != 0) {
                     const auto due = Clock::time_point(std::chrono::nanoseconds(t0)) + window;
                     if (Clock::now() >= due) {
-                        // The window is over; seal only when a free slot can
-                        // take over at once.  With every other slot still on
-                        // the GPU the batch could not start earlier anyway:
-                        // it keeps filling (larger batches under load, no
-                        // producer blocked) until a slot is returned (the
-                        // completer notifies), it is full, or a flush.
-                        if (!free_slots.empty()) { why = kSealTimer; break; }
-                        cv_flusher.wait_for(lk, std::chrono::milliseconds(50));
-                        continue;
+                        why = kSealTimer;
+                        break;
                     }
                     cv_flusher.wait_until(lk, due);
                 } else {
@@ -403,7 +396,6 @@ void lcb_hash_queue_s::completer_main() {
             free_slots.push_back(b);
         }
         cv_free.notify_one();
-        cv_flusher.notify_one();   // a batch held open for want of a slot may go now
         cv_done.notify_all();
     }
 }
@@ -436,7 +428,22 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     b.meta = new (std::nothrow) Meta[msgs];
     b.leases = new (std::nothrow) LeaseRec[nleases];
     b.nleases = nleases;
-    return (b.meta && b.leases) ? 0 : ENOMEM;
+    if (!b.meta || !b.leases) return ENOMEM;
+    // Touch every buffer once through the path a batch takes (host arena ->
+    // HBM by DMA, digests back): first use of fresh device pages and DMA
+    // mappings cost milliseconds, which would otherwise land on the first
+    // full-size batches' packets.
+    memset(b.h_off, 0, msgs * 8);
+    memset(b.h_len, 0, msgs * 4);
+    if (hipMemcpyAsync(b.d_data, b.h_data, bytes, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+        hipMemcpyAsync(b.d_off, b.h_off, msgs * 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+        hipMemcpyAsync(b.d_len, b.h_len, msgs * 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+        hipMemsetAsync(b.d_dig, 0, msgs * D, b.stream) != hipSuccess ||
+        hipMemsetAsync(b.d_work, 0, (kLenClasses + 1 + msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
+        hipMemcpyAsync(b.h_dig, b.d_dig, msgs * D, hipMemcpyDeviceToHost, b.stream) != hipSuccess ||
+        hipStreamSynchronize(b.stream) != hipSuccess)
+        return EIO;
+    return 0;
 }
 
 void free_slot(Slot& b) {

@@ -145,15 +145,21 @@ int main(int argc, char** argv) {
     }
 
     lcb_hash_queue_p q = nullptr;
-    int rc = lcb_hash_queue_create(alg, key.empty() && keyhex.empty() ? nullptr : key.data(), key.size(), &cfg, &q);
+    const uint8_t* kp = key.empty() && keyhex.empty() ? nullptr : key.data();
+    int rc = lcb_hash_queue_create(alg, kp, key.size(), &cfg, &q);
     if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
 
-    // Warm-up: one batch through the whole pipeline (first launch, clocks).
+    // Warm-up on a throwaway queue: batches through the whole pipeline (first
+    // launches, clocks), so the measured queue's stats hold the run alone.
     {
-        std::vector<uint8_t> wd(std::min<uint64_t>(packets, 4096) * D);
+        std::vector<uint8_t> wd(std::min<uint64_t>(packets, 16384) * D);
         for (uint64_t i = 0; i < wd.size() / D; ++i)
             lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &wd[i * D], nullptr, nullptr, 0);
         lcb_hash_queue_wait(q);
+        lcb_hash_queue_destroy(q);
+        q = nullptr;
+        rc = lcb_hash_queue_create(alg, kp, key.size(), &cfg, &q);
+        if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
     }
     lcb_hash_queue_stats_t st0;
     lcb_hash_queue_stats(q, &st0);
