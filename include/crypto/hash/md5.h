@@ -72,32 +72,39 @@ md5_transform(md5_ctx_p ctx, const uint8_t *block) {
 		0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391
 	};
 	static const uint8_t S[16] = { 7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21 };
-	uint32_t x[16], v[4], f, t;
+	uint32_t x[16], v[4], a, t;
 	size_t i, g;
 
-	for (i = 0; i < 16; i ++) {	/* little-endian words */
-		x[i] = ((uint32_t)block[4 * i]) | ((uint32_t)block[4 * i + 1] << 8) |
-		    ((uint32_t)block[4 * i + 2] << 16) | ((uint32_t)block[4 * i + 3] << 24);
+	memcpy(x, block, sizeof(x));	/* little-endian words, any alignment */
+#if defined(__BYTE_ORDER__) && (__BYTE_ORDER__ == __ORDER_BIG_ENDIAN__)
+	for (i = 0; i < 16; i ++) {
+		x[i] = __builtin_bswap32(x[i]);
 	}
+#endif
 	memcpy(v, ctx->hash, sizeof(v));
 	/* Four 16-step rounds, each a loop the compiler fully unrolls so the
-	 * word index, constant and rotation fold to immediates. */
-#define MD5_ROUND(__r, __f, __g) do {						\
+	 * word index, constant and rotation fold to immediates.  Each step
+	 * starts from a + (x[g] + T[i]), which does not wait for the previous
+	 * step, so only the round function, one add, the rotate and the add of
+	 * b sit on the chain; round 2's G is added as its two disjoint terms
+	 * (c & ~d) + (b & d), the first of which does not wait for b either. */
+#define MD5_ROUND(__r, __g, __fn) do {						\
 	_Pragma("GCC unroll 16")						\
 	for (i = 16 * (__r); i < 16 * (__r) + 16; i ++) {			\
-		f = (__f);							\
 		g = (__g);							\
+		a = v[0] + (x[g] + T[i]);					\
+		__fn;								\
 		t = v[3];							\
 		v[3] = v[2];							\
 		v[2] = v[1];							\
-		v[1] += md5_rol32((v[0] + f + x[g] + T[i]), S[4 * (__r) + (i & 3)]); \
+		v[1] += md5_rol32(a, S[4 * (__r) + (i & 3)]);			\
 		v[0] = t;							\
 	}									\
 } while (0)
-	MD5_ROUND(0, (v[3] ^ (v[1] & (v[2] ^ v[3]))), i);
-	MD5_ROUND(1, (v[2] ^ (v[3] & (v[1] ^ v[2]))), ((5 * i + 1) & 15));
-	MD5_ROUND(2, (v[1] ^ v[2] ^ v[3]), ((3 * i + 5) & 15));
-	MD5_ROUND(3, (v[2] ^ (v[1] | ~v[3])), ((7 * i) & 15));
+	MD5_ROUND(0, i, a += (v[3] ^ (v[1] & (v[2] ^ v[3]))));
+	MD5_ROUND(1, ((5 * i + 1) & 15), (a += (v[2] & ~v[3]), a += (v[1] & v[3])));
+	MD5_ROUND(2, ((3 * i + 5) & 15), a += (v[1] ^ v[2] ^ v[3]));
+	MD5_ROUND(3, ((7 * i) & 15), a += (v[2] ^ (v[1] | ~v[3])));
 #undef MD5_ROUND
 	for (i = 0; i < 4; i ++) {
 		ctx->hash[i] += v[i];

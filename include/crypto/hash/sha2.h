@@ -56,8 +56,15 @@ static const uint64_t SHA2_512_H0[8] = {
 	0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull };
 
 #define SHA2_ALIGN(__n)	__attribute__ ((aligned(__n)))
-#if defined(__SHA__) && defined(__SSSE3__) && defined(__SSE4_1__)
-#	define SHA2_ENABLE_SIMD	1	/* layout only: this header has no SIMD path */
+#if defined(__SHA__) && defined(__SSSE3__) && defined(__SSE4_1__) && \
+    (defined(__x86_64__) || defined(__i386__))
+/* Built with the SHA extensions enabled (as the reference's SIMD build):
+ * SHA-224/256 blocks go through the SHA-NI instructions when the CPU has
+ * them (checked once per context by sha2_init, like the reference's
+ * use_simd). */
+#	define SHA2_ENABLE_SIMD	1
+#	include <immintrin.h>
+#	include <cpuid.h>
 #endif
 
 /* Field for field the reference's layout (sha2.h:152-163), including the
@@ -71,7 +78,7 @@ typedef struct sha2_ctx_s {
 	size_t hash_size;	/* 28, 32, 48 or 64 (0: invalid bits) */
 	size_t block_size;	/* 64 or 128 */
 #ifdef SHA2_ENABLE_SIMD
-	int use_simd;		/* layout only */
+	int use_simd;		/* SHA-NI available (sha2_init) */
 #endif
 } sha2_ctx_t, *sha2_ctx_p;
 
@@ -103,6 +110,27 @@ sha2_load_be(const uint8_t *p, const size_t n) {
 	return (v);
 }
 
+#ifdef SHA2_ENABLE_SIMD
+/* SHA-NI usable on this CPU (SHA, SSSE3, SSE4.1). */
+static inline int
+sha2_cpu_has_sha_ni(void) {
+#if defined(__GNUC__) && !defined(__clang__) && (__GNUC__ >= 11)
+	/* libgcc's cpu model, filled in at program start: no cpuid per call. */
+	return (__builtin_cpu_supports("sha") && __builtin_cpu_supports("ssse3") &&
+	    __builtin_cpu_supports("sse4.1"));
+#else
+	unsigned int a, b, c, d;
+
+	if (0 == __get_cpuid(1, &a, &b, &c, &d) ||
+	    0 == (c & (1u << 9)) || 0 == (c & (1u << 19)))	/* SSSE3, SSE4.1 */
+		return (0);
+	if (0 == __get_cpuid_count(7, 0, &a, &b, &c, &d))
+		return (0);
+	return (0 != (b & (1u << 29)));				/* SHA */
+#endif
+}
+#endif
+
 static inline void
 sha2_init(const size_t bits, sha2_ctx_p ctx) {
 
@@ -133,6 +161,9 @@ sha2_init(const size_t bits, sha2_ctx_p ctx) {
 		memcpy(ctx->hash, SHA2_512_H0, sizeof(SHA2_512_H0));
 		break;
 	}
+#ifdef SHA2_ENABLE_SIMD
+	ctx->use_simd = sha2_cpu_has_sha_ni();
+#endif
 }
 
 static inline void
@@ -147,13 +178,14 @@ sha2_transform_block64(sha2_ctx_p ctx, const uint8_t *blk) {
 		0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
 		0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2
 	};
-	uint32_t *h = (uint32_t*)ctx->hash, w[16], s[8], t1, t2, x, y;
+	uint32_t *h = (uint32_t*)ctx->hash, w[16], s[8], t1, t2, x, y, ab, bc;
 	size_t i;
 
 	for (i = 0; i < 16; i ++) {
 		w[i] = (uint32_t)sha2_load_be(blk + 4 * i, 4);
 	}
 	memcpy(s, h, sizeof(s));
+	bc = (s[1] ^ s[2]);
 #pragma GCC unroll 64
 	for (i = 0; i < 64; i ++) {
 		if (i >= 16) {
@@ -163,10 +195,14 @@ sha2_transform_block64(sha2_ctx_p ctx, const uint8_t *blk) {
 			    w[(i + 9) & 15] +
 			    (sha2_ror32(y, 17) ^ sha2_ror32(y, 19) ^ (y >> 10)));
 		}
-		t1 = (s[7] + (sha2_ror32(s[4], 6) ^ sha2_ror32(s[4], 11) ^ sha2_ror32(s[4], 25)) +
-		    (s[6] ^ (s[4] & (s[5] ^ s[6]))) + K[i] + w[i & 15]);
+		/* h + K + W does not wait for this round's e; Maj(a, b, c) =
+		 * b ^ ((a ^ b) & (b ^ c)), and a ^ b is the next round's b ^ c. */
+		t1 = ((s[7] + (K[i] + w[i & 15])) + (s[6] ^ (s[4] & (s[5] ^ s[6]))) +
+		    (sha2_ror32(s[4], 6) ^ sha2_ror32(s[4], 11) ^ sha2_ror32(s[4], 25)));
+		ab = (s[0] ^ s[1]);
 		t2 = ((sha2_ror32(s[0], 2) ^ sha2_ror32(s[0], 13) ^ sha2_ror32(s[0], 22)) +
-		    ((s[0] & s[1]) | (s[2] & (s[0] | s[1]))));
+		    (s[1] ^ (ab & bc)));
+		bc = ab;
 		s[7] = s[6]; s[6] = s[5]; s[5] = s[4]; s[4] = s[3] + t1;
 		s[3] = s[2]; s[2] = s[1]; s[1] = s[0]; s[0] = (t1 + t2);
 	}
@@ -199,13 +235,14 @@ sha2_transform_block128(sha2_ctx_p ctx, const uint8_t *blk) {
 		0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
 		0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull
 	};
-	uint64_t *h = ctx->hash, w[16], s[8], t1, t2, x, y;
+	uint64_t *h = ctx->hash, w[16], s[8], t1, t2, x, y, ab, bc;
 	size_t i;
 
 	for (i = 0; i < 16; i ++) {
 		w[i] = sha2_load_be(blk + 8 * i, 8);
 	}
 	memcpy(s, h, sizeof(s));
+	bc = (s[1] ^ s[2]);
 #pragma GCC unroll 80
 	for (i = 0; i < 80; i ++) {
 		if (i >= 16) {
@@ -215,10 +252,12 @@ sha2_transform_block128(sha2_ctx_p ctx, const uint8_t *blk) {
 			    w[(i + 9) & 15] +
 			    (sha2_ror64(y, 19) ^ sha2_ror64(y, 61) ^ (y >> 6)));
 		}
-		t1 = (s[7] + (sha2_ror64(s[4], 14) ^ sha2_ror64(s[4], 18) ^ sha2_ror64(s[4], 41)) +
-		    (s[6] ^ (s[4] & (s[5] ^ s[6]))) + K[i] + w[i & 15]);
+		t1 = ((s[7] + (K[i] + w[i & 15])) + (s[6] ^ (s[4] & (s[5] ^ s[6]))) +
+		    (sha2_ror64(s[4], 14) ^ sha2_ror64(s[4], 18) ^ sha2_ror64(s[4], 41)));
+		ab = (s[0] ^ s[1]);
 		t2 = ((sha2_ror64(s[0], 28) ^ sha2_ror64(s[0], 34) ^ sha2_ror64(s[0], 39)) +
-		    ((s[0] & s[1]) | (s[2] & (s[0] | s[1]))));
+		    (s[1] ^ (ab & bc)));	/* Maj, as in the 64-byte block */
+		bc = ab;
 		s[7] = s[6]; s[6] = s[5]; s[5] = s[4]; s[4] = s[3] + t1;
 		s[3] = s[2]; s[2] = s[1]; s[1] = s[0]; s[0] = (t1 + t2);
 	}
@@ -227,12 +266,73 @@ sha2_transform_block128(sha2_ctx_p ctx, const uint8_t *blk) {
 	}
 }
 
+#ifdef SHA2_ENABLE_SIMD
+/* SHA-224/256 blocks with the SHA-NI instructions.  The state is kept as
+ * the two lane groups the instructions use, {A, B, E, F} and {C, D, G, H};
+ * each sha256rnds2 does two rounds, the message schedule four words at a
+ * time (sha256msg1: W[t-16] + sigma0(W[t-15]); + W[t-7]; sha256msg2 adds
+ * sigma1 of the last two words). */
+__attribute__((target("sha,ssse3,sse4.1")))
+static inline void
+sha2_transform_block64_shani(sha2_ctx_p ctx, const uint8_t *blocks, const uint8_t *blocks_max) {
+	static const uint32_t K4[64] SHA2_ALIGN(16) = {
+		0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+		0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+		0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+		0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+		0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+		0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+		0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+		0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2
+	};
+	const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bll, 0x0405060700010203ll);
+	uint32_t *h = (uint32_t*)ctx->hash;
+	__m128i t, abef, cdgh, abef0, cdgh0, wk, m[4];
+	size_t g;
+
+	t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)(const void*)&h[0]), 0xb1);	/* C D A B */
+	cdgh = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)(const void*)&h[4]), 0x1b);	/* H G F E */
+	abef = _mm_alignr_epi8(t, cdgh, 8);						/* A B E F */
+	cdgh = _mm_blend_epi16(cdgh, t, 0xf0);						/* C D G H */
+	for (; blocks < blocks_max; blocks += SHA2_256_MSG_BLK_SIZE) {
+		abef0 = abef;
+		cdgh0 = cdgh;
+#pragma GCC unroll 16
+		for (g = 0; g < 16; g ++) {	/* four rounds per step */
+			if (g < 4) {
+				m[g] = _mm_shuffle_epi8(_mm_loadu_si128(
+				    (const __m128i*)(const void*)(blocks + 16 * g)), bswap);
+			} else {
+				m[g & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(
+				    _mm_sha256msg1_epu32(m[g & 3], m[(g + 1) & 3]),
+				    _mm_alignr_epi8(m[(g + 3) & 3], m[(g + 2) & 3], 4)), m[(g + 3) & 3]);
+			}
+			wk = _mm_add_epi32(m[g & 3], _mm_load_si128((const __m128i*)(const void*)&K4[4 * g]));
+			cdgh = _mm_sha256rnds2_epu32(cdgh, abef, wk);
+			abef = _mm_sha256rnds2_epu32(abef, cdgh, _mm_shuffle_epi32(wk, 0x0e));
+		}
+		abef = _mm_add_epi32(abef, abef0);
+		cdgh = _mm_add_epi32(cdgh, cdgh0);
+	}
+	t = _mm_shuffle_epi32(abef, 0x1b);					/* F E B A */
+	cdgh = _mm_shuffle_epi32(cdgh, 0xb1);					/* D C H G */
+	_mm_storeu_si128((__m128i*)(void*)&h[0], _mm_blend_epi16(t, cdgh, 0xf0));	/* D C B A */
+	_mm_storeu_si128((__m128i*)(void*)&h[4], _mm_alignr_epi8(cdgh, t, 8));	/* H G F E */
+}
+#endif
+
 /* Compress every block in [blocks, blocks_max) (any alignment). */
 static inline void
 sha2_transform(sha2_ctx_p ctx, const uint8_t *blocks, const uint8_t *blocks_max) {
 
 	if (0 == ctx->block_size)
 		return;
+#ifdef SHA2_ENABLE_SIMD
+	if (0 != ctx->use_simd && SHA2_256_MSG_BLK_SIZE == ctx->block_size) {
+		sha2_transform_block64_shani(ctx, blocks, blocks_max);
+		return;
+	}
+#endif
 	for (; blocks < blocks_max; blocks += ctx->block_size) {
 		if (SHA2_256_MSG_BLK_SIZE == ctx->block_size) {
 			sha2_transform_block64(ctx, blocks);

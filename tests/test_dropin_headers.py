@@ -28,9 +28,16 @@ def build(tmp_path, src, out, extra=(), inc=(INC,)):
     return exe
 
 
-@pytest.fixture(scope="module")
-def driver(tmp_path_factory):
-    return build(tmp_path_factory.mktemp("dropin"), os.path.join(C, "dropin_driver.c"), "drv")
+SIMD_FLAGS = ["-msse4.1", "-mssse3", "-msha", "-mavx2"]
+
+
+@pytest.fixture(scope="module", params=["generic", "simd"])
+def driver(tmp_path_factory, request):
+    """The KAT driver built plain, and with the SHA extensions enabled (the
+    reference's SIMD build flags): SHA-224/256 then run on SHA-NI when the
+    CPU has it (sha2.h sha2_transform_block64_shani)."""
+    return build(tmp_path_factory.mktemp("dropin"), os.path.join(C, "dropin_driver.c"), "drv",
+                 extra=SIMD_FLAGS if request.param == "simd" else ())
 
 
 def run_driver(exe, lines):
