@@ -767,12 +767,15 @@ struct GatherLineStream : LdsLineStream {
     // re-reads its last line; the data is discarded).  Pointers advance in
     // place: no per-issue address temporaries next to the line in VGPRs.
     // All records have the same number of lines: no clamping, no rem[].
+    // kAux: cache policy (kGatherAux, or kLdsAux when every streamed line is a
+    // whole 128-B cache line read once).
+    template <int kAux = kGatherAux>
     __device__ __forceinline__ void issue_next_uniform() {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[g],
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
-                                             kGatherAux);
+                                             kAux);
             src[g] += 128;
         }
     }

@@ -197,14 +197,38 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, uint64_t first, u
     uint64_t done = 0;
     if (__all(ok)) {  // wave-uniform
         const uint32_t nlu = (uint32_t)__builtin_amdgcn_readfirstlane(nl);
+        // Half-line phase of the tile (bucketing groups it): 0 when every
+        // record starts on a 128-B line, 1 when every record starts 64 B into
+        // one, 2 otherwise.
+        const uint32_t ma = (uint32_t)reinterpret_cast<uintptr_t>(msg) & 127u;
+        const uint32_t ma0 = (uint32_t)__builtin_amdgcn_readfirstlane(ma);
+        const uint32_t ph = (__all(ma == ma0) && (ma0 & 63u) == 0) ? (ma0 >> 6) : 2u;
         GatherLineStream gs;
-        gs.init_gather(msg, nlu - 1, lane, slab);
-        gs.issue_next_uniform();
-        for (uint32_t L = 0; L < nlu; ++L) {
-            uint32_t w[32];
-            gs.take(w, w + 16);
-            if (L + 1 < nlu) gs.issue_next_uniform();
-            md_compress_line(st, w);
+        if (H::kBlock == 64 && ph < 2) {
+            // Whole cache lines: a 64-B-phase tile streams the nlu + 1 lines
+            // its records overlap (line L = blocks 2L-1 and 2L of the record;
+            // the bytes before its first block and after its last whole line
+            // share those cache lines and are discarded), so no line is read
+            // twice and the stream carries the read-once (nt) policy.
+            const uint32_t n = nlu + ph;
+            gs.init_gather(msg - 64 * ph, n - 1, lane, slab);
+            gs.issue_next_uniform<kLdsAux>();
+            for (uint32_t L = 0; L < n; ++L) {
+                uint32_t w[32];
+                gs.take(w, w + 16);
+                if (L + 1 < n) gs.issue_next_uniform<kLdsAux>();
+                if (ph == 0 || L > 0) st.compress(w);
+                if (ph == 0 || L < nlu) st.compress(w + 16);
+            }
+        } else {
+            gs.init_gather(msg, nlu - 1, lane, slab);
+            gs.issue_next_uniform();
+            for (uint32_t L = 0; L < nlu; ++L) {
+                uint32_t w[32];
+                gs.take(w, w + 16);
+                if (L + 1 < nlu) gs.issue_next_uniform();
+                md_compress_line(st, w);
+            }
         }
         done = (uint64_t)nlu * 128;
     }
@@ -581,69 +605,76 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t seed, uint64_t start,
 // (a counting sort; order inside a class is arbitrary and does not affect
 // any digest, which is always written at the message's own index).
 //   class(len) = nb for nb = len/64 + 1 < 64, else 58 + floor(log2(nb))
-// i.e. exact block counts up to 4 KiB, power-of-two bins above.
+// i.e. exact block counts up to 4 KiB, power-of-two bins above.  Inside a
+// class, records whose start lies in the first half of a 128-B line come
+// after those in the second half (key = class * 2 + half): tiles of 64
+// consecutive entries then share their half-line phase, and the tile kernel
+// streams a 64-B-phase tile as whole cache lines (md_tile_stream).
 __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     const uint64_t nb = (len >> 6) + 1;
     if (nb < 64) return (uint32_t)nb;
     return 58u + (63u - (uint32_t)__clzll((long long)nb));
 }
 
-__global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t* lengths, uint64_t count,
-                                                          uint32_t* hist) {
-    __shared__ uint32_t h[kLenClasses];
-    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x) h[c] = 0;
+__device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
+    const uint64_t off = a.offsets ? gptr(a.offsets)[i] : i * a.stride;
+    const uint32_t half = (uint32_t)(((reinterpret_cast<uintptr_t>(a.data) + off) >> 6) & 1u);
+    return (len_class(gptr(a.lengths)[i]) << 1) | half;
+}
+
+__global__ __launch_bounds__(256) void bucket_hist_kernel(KArgs a, uint32_t* hist) {
+    __shared__ uint32_t h[kBucketKeys];
+    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
          i += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[len_class(lengths[i])], 1u);
+        atomicAdd(&h[bucket_key(a, i)], 1u);
     __syncthreads();
-    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x)
+    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x)
         if (h[c]) atomicAdd(&hist[c], h[c]);
 }
 
-// Exclusive prefix over classes in DESCENDING class order -> start cursor.
+// Exclusive prefix over keys in DESCENDING key order -> start cursor.
 __global__ void bucket_scan_kernel(uint32_t* hist_to_cursor) {
     if (threadIdx.x != 0) return;
     uint32_t run = 0;
-    for (int c = kLenClasses - 1; c >= 0; --c) {
+    for (int c = kBucketKeys - 1; c >= 0; --c) {
         const uint32_t n = hist_to_cursor[c];
         hist_to_cursor[c] = run;
         run += n;
     }
 }
 
-// Each block reserves a contiguous range per class with one global atomic,
+// Each block reserves a contiguous range per key with one global atomic,
 // then scatters its indices (LDS atomics give the in-block rank).
-__global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t* lengths, uint64_t count,
-                                                             uint32_t* cursor, uint32_t* order) {
-    __shared__ uint32_t h[kLenClasses];
-    __shared__ uint32_t base[kLenClasses];
-    for (int c = threadIdx.x; c < kLenClasses; c += blockDim.x) h[c] = 0;
+__global__ __launch_bounds__(256) void bucket_scatter_kernel(KArgs a, uint32_t* cursor, uint32_t* order) {
+    __shared__ uint32_t h[kBucketKeys];
+    __shared__ uint32_t base[kBucketKeys];
+    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t c = 0, r = 0;
-    if (i < count) {
-        c = len_class(lengths[i]);
+    if (i < a.count) {
+        c = bucket_key(a, i);
         r = atomicAdd(&h[c], 1u);
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < kLenClasses; k += blockDim.x)
+    for (int k = threadIdx.x; k < kBucketKeys; k += blockDim.x)
         base[k] = h[k] ? atomicAdd(&cursor[k], h[k]) : 0u;
     __syncthreads();
-    if (i < count) order[base[c] + r] = (uint32_t)i;
+    if (i < a.count) order[base[c] + r] = (uint32_t)i;
 }
 
-void launch_bucketing(const uint32_t* lengths, uint64_t count, uint32_t* work, uint32_t* order,
-                      hipStream_t s) {
-    // work: kLenClasses class cursors + the tile-queue head, zeroed here;
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream_t s) {
+    // work: kBucketKeys key cursors + the tile-queue head, zeroed here;
     // order: count uint32.
-    (void)hipMemsetAsync(work, 0, (kLenClasses + 1) * sizeof(uint32_t), s);
-    uint64_t hb = (count + 255) / 256;
+    (void)hipMemsetAsync(work, 0, (kBucketKeys + 1) * sizeof(uint32_t), s);
+    uint64_t hb = (a.count + 255) / 256;
     if (hb > 2048) hb = 2048;
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)hb), dim3(256), 0, s, lengths, count, work);
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)hb), dim3(256), 0, s, a, work);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(64), 0, s, work);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s,
-                       lengths, count, work, order);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, s, a, work,
+                       order);
 }
 
 // ------------------------------------------------------------- launchers

@@ -252,9 +252,9 @@ def test_bucketed_equals_unbucketed(gpu, oracle):
 @pytest.mark.parametrize("layout", ["aligned16", "packed", "mostly_aligned"])
 def test_ragged_line_stream(gpu, oracle, layout):
     """Bucketed ragged batches (count above the bucketing threshold) take the
-    LDS line-stream gather kernel (md_gather_lds_kernel): waves whose records
-    all start 16-B aligned stream their whole lines through LDS, the others
-    fall back per wave.  Lengths 0..3000 plus a few 64 KiB records, so waves
+    persistent tile kernel (md_tiles_kernel): tiles whose records all start
+    16-B aligned with equal line counts stream their lines through LDS, the
+    others load per lane.  Lengths 0..3000 plus a few 64 KiB records, so waves
     mix records with and without whole lines; plain and HMAC."""
     rng = np.random.default_rng(len(layout))
     n = 6000
@@ -275,6 +275,42 @@ def test_ragged_line_stream(gpu, oracle, layout):
             exp = oracle.batch(alg, data, offs, lens, key=key)
             got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=key).cpu().numpy()
             assert np.array_equal(got, exp), (alg, layout, key is not None)
+
+
+@pytest.mark.parametrize("mix", ["halves", "all64", "any16"])
+def test_ragged_half_line_phase(gpu, oracle, mix):
+    """Bucketed ragged batches whose records start 0 or 64 B into a 128-B line
+    (packed 64-B multiples, as C4): the bucketing groups each length class by
+    that half-line phase and the tile kernel streams a 64-B-phase tile as the
+    whole cache lines its records overlap (first and last line half
+    discarded).  Lengths of whole lines, whole lines + 64 and ragged tails;
+    the last record ends at the end of the buffer; other 16-B phases ("any16")
+    keep the record-relative stream.  MD5 plain and HMAC (the tile kernel's
+    algorithm) plus SHA-256 and GOST through the same bucketing."""
+    rng = np.random.default_rng({"halves": 1, "all64": 2, "any16": 3}[mix])
+    n = 6000
+    lines = rng.integers(1, 40, n)
+    tail = rng.choice([0, 64, 0, 17, 100], n)
+    lens = (128 * lines + tail).astype(np.uint32)
+    lens[rng.integers(0, n, 30)] = 65536
+    lens[-1] = 128 * 7
+    offs = np.zeros(n, np.uint64)
+    pos = 64 if mix == "all64" else 0
+    for k in range(n):
+        if mix == "all64":
+            pos = (pos + 63) // 128 * 128 + 64
+        elif mix == "halves":
+            pos = (pos + 63) // 64 * 64
+        else:
+            pos = (pos + 15) // 16 * 16
+        offs[k] = pos
+        pos += int(lens[k])
+    data = gen_stream(5, pos)
+    dd, dl, do = dev(data), dev(lens, np.int32), dev(offs, np.int64)
+    for alg, key in ((1, None), (1, b"radius-secret"), (4, None), (7, None)):
+        exp = oracle.batch(alg, data, offs, lens, key=key)
+        got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=key).cpu().numpy()
+        assert np.array_equal(got, exp), (alg, mix, key is not None)
 
 
 def test_host_mode_pinned_direct_dma(gpu, batches):
