@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void crc_batch_kernel(KArgs a) {
 }
 
 // Fixed-stride batches (lcb_internal.hpp fixed_stride_lines): the 128-B lines
-// arrive through the per-wave LDS-DMA line stream (LdsLineStream,
+// arrive through the per-wave LDS-DMA line stream (LdsStridedStream,
 // hash_device.hpp), line L+1 in flight while line L is folded in.
 template <int V>
 __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
@@ -38,14 +38,19 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     __shared__ uint32_t T[8 * 256];
     __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
     crc_stage_tables(T, Var::kFam);  // before any early return: it synchronises
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
+    // A partial last wave moves back over its predecessor's records (count
+    // >= 64) and stores only its own.
     const uint64_t last = a.count - 1, nlines = a.fixed_len / 128;
-    LdsLineStream ls;
-    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
-    const uint64_t i = wave_first + lane, ic = i > last ? last : i;
-    const uint32_t c = a.init ? gptr(a.init)[ic] : Var::kOneshot;
+    const uint32_t skip = wave_first + 63 > last ? (uint32_t)(wave_first + 63 - last) : 0u;
+    wave_first -= skip;
+    LdsStridedStream ls;
+    ls.init(a.data, a.stride, wave_first, lane, &slab[wv][0]);
+    const uint64_t i = wave_first + lane;
+    const uint32_t c = a.init ? gptr(a.init)[i] : Var::kOneshot;
     const CrcRule<Var::kRefl> R{T};
     uint32_t r = Var::kInv ? ~c : c;
     if (nlines) ls.issue(0);
@@ -58,7 +63,7 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) r = R.step8(r, w1[2 * j], w1[2 * j + 1]);
     }
-    if (i > last) return;
+    if (lane < skip) return;
     r = crc_message(R, r, gptr(a.data) + i * a.stride + nlines * 128, (uint64_t)a.fixed_len - nlines * 128);
     gptr(reinterpret_cast<uint32_t*>(a.digests))[i] = Var::kInv ? ~r : r;
 }

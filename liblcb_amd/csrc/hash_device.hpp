@@ -683,42 +683,23 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // VGPRs (take), and the caller issues line L+1 before computing line L.
 // 16-B chunks are XOR-swizzled (chunk k of local record j sits in slot
 // k ^ ((j >> 1) & 7)) so the 16-lane ds_read_b128 groups are conflict-free.
-// Lanes beyond the last record load the last record (clamped) and must not
-// store.  The DMA stream carries the nt cache policy (every byte is read
-// once; kLdsAux).
-// Cache policy of the ragged (gather) line stream: default.  Records of a
+// The fixed-stride stream (LdsStridedStream) always covers 64 whole records;
+// the ragged one (GatherLineStream) repeats a record's last line once it has
+// run out.  The fixed-stride DMA carries the nt cache policy (every byte is
+// read once; kLdsAux).
+// Default cache policy of the ragged (gather) line stream: a record of a
 // packed ragged batch need not start on a 128-B line, so one streamed "line"
-// spans two cache lines; with nt the second is gone before the record's next
-// line asks for it (64 KiB records at a 64-B phase: 5.95 ms with nt, 4.70
-// default; profiles/r2_c4_tiles_ab.txt).
+// can span two cache lines; with nt the second is gone before the record's
+// next line asks for it (64 KiB records at a 64-B phase: 5.95 ms with nt,
+// 4.70 default; profiles/r2_c4_tiles_ab.txt).  Tiles whose records share
+// a 0 or 64-B phase stream whole cache lines with nt instead (md_tile_stream).
 constexpr int kGatherAux = 0;
 constexpr int kLdsAux = 2;  // cache policy of the LDS-DMA stream: nt (every byte is read once)
-struct LdsLineStream {
-    const uint8_t* src[8];
+// The slab side shared by the line streams: take() copies this lane's 128 B
+// of the landed line into VGPRs.
+struct LdsLineSlab {
     uint8_t* slab;
     uint32_t lane;
-    __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first,
-                                         uint64_t last, uint32_t ln, uint8_t* my_slab) {
-        lane = ln;
-        slab = my_slab;
-        // DMA sources: instruction g carries local records 8g .. 8g+7; this lane
-        // moves chunk ((lane & 7) ^ f) of record 8g + (lane >> 3), f = (4g + (lane >> 4)) & 7.
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            uint64_t j = wave_first + 8 * g + (lane >> 3);
-            j = j > last ? last : j;
-            const uint32_t f = ((lane >> 4) + 4 * g) & 7;
-            src[g] = data + j * stride + ((lane & 7) ^ f) * 16;
-        }
-    }
-    // Line L into slab buffer `buf` (8 KiB each; one buffer per line in flight).
-    __device__ __forceinline__ void issue(uint64_t L, uint32_t buf = 0) const {
-#pragma unroll
-        for (int g = 0; g < 8; ++g)
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[g] + L * 128),
-                                             (__attribute__((address_space(3))) void*)(slab + buf * 8192 + g * 1024),
-                                             16, 0, kLdsAux);
-    }
     // Waits for the issued line, copies this lane's 128 B of buffer `buf`
     // (raw LE words); the buffer is free again on return.
     __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16], uint32_t buf = 0) const {
@@ -743,11 +724,53 @@ struct LdsLineStream {
     }
 };
 
+// Fixed-stride stream with a wave-uniform base: instruction g of line L reads
+// from (wave base + 8 g stride + 128 L) — a scalar address — plus one of two
+// per-lane 32-bit offsets (record lane >> 3 and the chunk, for even and odd
+// g), i.e. the saddr form of global_load_lds with 2 VGPRs of addressing
+// instead of 8 64-bit pointers.  The wave covers 64 whole records (the caller
+// shifts a partial last wave back over its predecessor's records), so there
+// is no per-lane clamp.  Needs 7 * stride + 128 < 2^32.
+struct LdsStridedStream : LdsLineSlab {
+    const uint8_t* wbase;   // wave-uniform
+    uint64_t stride8;       // wave-uniform: 8 records
+    uint32_t voff[2];
+    __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first, uint32_t ln,
+                                         uint8_t* my_slab) {
+        lane = ln;
+        slab = my_slab;
+        wbase = data + wave_first * stride;
+        stride8 = 8 * stride;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const uint32_t f = ((ln >> 4) + 4 * p) & 7;
+            voff[p] = (ln >> 3) * (uint32_t)stride + ((ln & 7) ^ f) * 16;
+        }
+    }
+    __device__ __forceinline__ void issue(uint64_t L) {
+        // Offsets re-defined in place (no copy): zero-extended at each use, so
+        // every DMA takes the saddr + 32-bit vaddr form.
+        asm volatile("" : "+v"(voff[0]), "+v"(voff[1]));
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            // Opaque scalar: keeps the loop optimiser from turning the
+            // address into a per-lane 64-bit induction variable.
+            uint64_t so = (uint64_t)g * stride8 + L * 128;
+            asm volatile("" : "+s"(so));
+            const uint8_t* sb = wbase + so;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g & 1]),
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             kLdsAux);
+        }
+    }
+};
+
 // Ragged variant: record j of the wave streams from its own base pointer
 // (any 16-B aligned start), re-reading its last whole line once it runs out
 // (the data is discarded; every DMA stays inside the record).  Bases and
 // limits are exchanged across lanes once, at init.
-struct GatherLineStream : LdsLineStream {
+struct GatherLineStream : LdsLineSlab {
+    const uint8_t* src[8];  // instruction g: this lane's chunk of local record 8g + (lane >> 3)
     uint32_t rem[8];   // advances left: lines of the record after the current one
     __device__ __forceinline__ void init_gather(const uint8_t* base, uint32_t last_line, uint32_t ln,
                                                 uint8_t* my_slab) {

@@ -60,22 +60,29 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
 // ------------------------------------------- MD family, fixed-stride fast path
 // Fixed-stride batches with 16-B aligned records of >= 128 bytes (the bench
 // workload and any array of equal-size records): each wave streams line L+1
-// of its 64 records into LDS (LdsLineStream, hash_device.hpp) while the two
-// 64-B blocks of line L are compressed.  Bytes after the last whole line go
-// through the generic loader.  One line in flight per wave (8 KiB of LDS),
-// 4 waves per workgroup, 5 workgroups per CU (the whole 160 KiB); deeper
-// per-wave buffering and half-line stages measured slower
-// (profiles/r1_lds_depth_ab.txt, profiles/r1_lds_half_ab.txt).
+// of its 64 records into LDS (LdsStridedStream, hash_device.hpp: scalar base
+// + two per-lane offsets, no VALU per DMA) while the two 64-B blocks of line
+// L are compressed.  Bytes after the last whole line go through the generic
+// loader.  One line in flight per wave (8 KiB of LDS), 4 waves per workgroup,
+// 5 workgroups per CU (the whole 160 KiB); deeper per-wave buffering,
+// half-line stages and taking the next line mid-way through the current one
+// (two line registers sets: 4 waves/SIMD) measured slower
+// (profiles/r1_lds_depth_ab.txt, r1_lds_half_ab.txt, r2_fixed_stream_ab.txt).
 template <class H, bool kHmac>
 __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
+    // A partial last wave moves back over its predecessor's records (count >=
+    // 64, fixed_stride_lines) and stores only its own: no per-lane clamping.
     const uint64_t last = a.count - 1;
+    const uint32_t skip = wave_first + 63 > last ? (uint32_t)(wave_first + 63 - last) : 0u;
+    wave_first -= skip;
     const uint64_t nlines = a.fixed_len / 128;
-    LdsLineStream ls;
-    ls.init(a.data, a.stride, wave_first, last, lane, &slab[wv][0]);
+    LdsStridedStream ls;
+    ls.init(a.data, a.stride, wave_first, lane, &slab[wv][0]);
     H st;
     uint64_t prefix = 0;
     if (kHmac) {
@@ -96,8 +103,8 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
             st.compress(w + 16);
         }
     }
+    if (lane < skip) return;
     const uint64_t i = wave_first + lane;
-    if (i > last) return;
     const uint8_t* msg = a.data + i * a.stride + nlines * 128;
     const uint64_t tail = (uint64_t)a.fixed_len - nlines * 128;
     if (tail == 0)  // wave-uniform: schedule of the pad block on the SALU

@@ -165,6 +165,26 @@ def test_fixed_whole_block_lengths(gpu, oracle, stride_pad):
                 assert np.array_equal(got.cpu().numpy(), exp), (alg, L, stride, key is not None)
 
 
+@pytest.mark.parametrize("count", [63, 64, 65, 127, 1000, 4096 + 7])
+def test_fixed_stride_partial_last_wave(gpu, oracle, count):
+    """Fixed-stride LDS-stream kernels cover whole 64-record waves: a partial
+    last wave moves back over its predecessor's records and stores only its
+    own (63 records: the per-lane kernel).  Lengths of whole lines and with a
+    ragged tail, every MD algorithm plus CRC-32 and HMAC-MD5."""
+    from liblcb_amd.crc32 import crc32_batch
+    for stride, flen in ((1024, 1024), (1040, 1000), (256, 130)):
+        data = gen_stream(count * 7 + flen, count * stride)
+        dd = dev(data)
+        for alg in range(1, 9):
+            for key in ((None, b"k") if alg == 1 else (None,)):
+                exp = oracle.batch(alg, data, count=count, stride=stride, fixed_len=flen, key=key)
+                got = gpu.hash_batch(alg, dd, count=count, stride=stride, fixed_len=flen, key=key).cpu().numpy()
+                assert np.array_equal(got, exp), (alg, count, stride, flen, key)
+        exp = oracle.crc32_batch(3, data, count=count, stride=stride, fixed_len=flen)
+        got = crc32_batch(3, dd, count=count, stride=stride, fixed_len=flen).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, np.asarray(exp).view(np.uint32)), ("crc", count, stride, flen)
+
+
 def test_unaligned_digest_output(gpu, oracle):
     data = gen_stream(1, 64 * 100)
     for alg in (1, 2, 6, 7):
