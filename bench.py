@@ -210,6 +210,35 @@ def valu_floor_ms(alg, count):
     return n * VALU_CYCLES / (VALU_SIMDS * VALU_CLOCK_HZ) * 1e3
 
 
+def read_probes(data, count, steps=50, warmup=20):
+    """Achievable HBM read rate on this box, GB/s: the digest
+    kernels' own LDS-DMA line stream over the same records without the
+    compression ("records"), and plain coalesced 16-B loads over the same
+    bytes ("linear"); lcb_hash_gpu_read_probe, HIP events around each launch."""
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, mode in (("records", 0), ("linear", 1)):
+        sink = torch.empty(max(1, lib().lcb_hash_gpu_probe_sink_words(mode, count)), dtype=torch.int32,
+                           device="cuda")
+
+        def launch():
+            check(lib().lcb_hash_gpu_read_probe(mode, data.data_ptr(), count, MSG_LEN, MSG_LEN,
+                                                sink.data_ptr(), stream.cuda_stream))
+        for _ in range(warmup):
+            launch()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for e0, e1 in ev:
+            e0.record(stream)
+            launch()
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+        out[name + "_GBps"] = round(count * MSG_LEN / (ms * 1e-3) / 1e9, 1)
+        out[name + "_ms"] = round(ms, 4)
+        del sink
+    return out
+
+
 def affinity_cpus():
     try:
         return len(os.sched_getaffinity(0))
@@ -574,6 +603,16 @@ def main():
                      "valu_floor_ms": round(vfloor, 4) if vfloor else None,
                      "valu_frac": round(vfloor / kms, 4) if vfloor else None},
     }
+
+    if rank == 0 and world == 1 and not a.no_extras:
+        # Achievable read rate on this box next to the spec peak: the same
+        # records through the kernel's line stream without compression, and a
+        # plain linear read (not `value`; the fraction against spec stays `frac`).
+        pr = read_probes(data, count)
+        r = out["roofline"]
+        r["achievable"] = pr
+        r["frac_of_stream"] = round(achieved / pr["records_GBps"], 4)
+        r["frac_of_linear_read"] = round(achieved / pr["linear_GBps"], 4)
 
     if not a.no_gather:
         # RCCL digest gather to rank 0 (outside the timed region), then the

@@ -196,6 +196,22 @@ int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
 int	lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t *dev_out,
 	    size_t n, void *stream);
 
+/* Diagnostics: HBM read probe (achievable read bandwidth on
+ * the box, measured next to the digest kernels; no reference counterpart).
+ * Reads `count` records of `fixed_len` bytes at `stride` from device memory
+ * `dev_data` without hashing them.  mode LCB_PROBE_RECORDS: the LDS-DMA line
+ * stream of the fixed-stride digest kernels (fixed_len >= 128, stride and
+ * dev_data 16-B aligned, count >= 64); `dev_sink` receives count uint32.
+ * mode LCB_PROBE_LINEAR: coalesced 16-B loads over count * stride bytes
+ * (a multiple of 16); `dev_sink` receives lcb_hash_gpu_probe_sink_words()
+ * uint32.  Asynchronous on `stream`.  EINVAL on a shape the mode cannot
+ * read. */
+#define LCB_PROBE_RECORDS	0
+#define LCB_PROBE_LINEAR	1
+int	lcb_hash_gpu_read_probe(int mode, const uint8_t *dev_data, size_t count,
+	    uint64_t stride, uint32_t fixed_len, uint32_t *dev_sink, void *stream);
+size_t	lcb_hash_gpu_probe_sink_words(int mode, size_t count);
+
 /* Diagnostics: copies the 8 x 256 GOST LPS lookup table the kernels use
  * (generated from the RFC 6986 pi / A constants) to host memory `out`
  * (2048 uint64_t), so tests can pin it against the reference's

@@ -534,7 +534,7 @@ struct Sha512 {
     template <int i>
     __device__ __forceinline__ static void round(Vars& v) {
         u64p x;
-        if (i < 16) {
+        if constexpr (i < 16) {
             x = v.w[i];
         } else {
             const u64p w15 = v.w[(i - 15) & 15], w2 = v.w[(i - 2) & 15];

@@ -670,6 +670,32 @@ int lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t* dev_out, size
     return map_err(hipGetLastError());
 }
 
+size_t lcb_hash_gpu_probe_sink_words(int mode, size_t count) {
+    if (mode == LCB_PROBE_RECORDS) return count;
+    if (ensure_init()) return 0;
+    return (size_t)8 * device_cu_count() * 256;
+}
+
+int lcb_hash_gpu_read_probe(int mode, const uint8_t* dev_data, size_t count, uint64_t stride, uint32_t fixed_len,
+                            uint32_t* dev_sink, void* stream) {
+    if (int rc = ensure_init()) return rc;
+    if (!dev_data || !dev_sink || count == 0) return EINVAL;
+    KArgs a{};
+    a.data = dev_data;
+    a.count = count;
+    a.stride = stride;
+    a.fixed_len = fixed_len;
+    if (mode == LCB_PROBE_RECORDS) {
+        if (!fixed_stride_lines(a)) return EINVAL;
+    } else if (mode == LCB_PROBE_LINEAR) {
+        if ((count * stride) % 16 || (reinterpret_cast<uintptr_t>(dev_data) & 15u)) return EINVAL;
+    } else {
+        return EINVAL;
+    }
+    launch_probe(mode, a, dev_sink, reinterpret_cast<hipStream_t>(stream));
+    return map_err(hipGetLastError());
+}
+
 int lcb_hash_gpu_gost_table(uint64_t* out) {
     if (!out) return EINVAL;
     gost_table_host(out);

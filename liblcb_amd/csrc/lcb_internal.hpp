@@ -102,6 +102,10 @@ void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t
 // Key-table prep of a keyed batch: mid[k] for every key (kKeyHmac, kKeyPrefix).
 void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s);
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
+// HBM read probes (lcb_hash_gpu_read_probe): mode 0 = the fixed-stride line
+// stream alone over `a`'s records, mode 1 = linear coalesced read of
+// count * stride bytes; sink: one uint32 per record (0) / per thread (1).
+void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s);
 void gost_table_host(uint64_t* out);
 
 // Shared by the C-ABI TUs (lcb_hash_gpu.cpp).

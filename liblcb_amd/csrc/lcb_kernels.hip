@@ -604,6 +604,70 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t seed, uint64_t start,
     }
 }
 
+// ------------------------------------------------- HBM read probes
+// Achievable read bandwidth on the box, measured beside the
+// digest kernels by bench.py: no compression, the same bytes.
+//   records: md_fixed_lds_kernel's stream exactly (LdsStridedStream over
+//            fixed-stride records, 4 waves x 5 workgroups per CU, one line in
+//            flight per wave), each lane folding its 128 B into one word;
+//   linear:  plain coalesced 16-B-per-lane loads over the whole range, 4 in
+//            flight per lane, grid of 8 workgroups per CU (8 in flight
+//            measured slower: 5.3 against 5.6 TB/s).
+// One uint32 per record / per thread goes to `sink` so nothing is dead.
+__global__ __launch_bounds__(256) void probe_records_kernel(KArgs a, uint32_t* sink) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    if (wave_first >= a.count) return;
+    const uint64_t last = a.count - 1;
+    const uint32_t skip = wave_first + 63 > last ? (uint32_t)(wave_first + 63 - last) : 0u;
+    wave_first -= skip;
+    const uint64_t nlines = a.fixed_len / 128;
+    LdsStridedStream ls;
+    ls.init(a.data, a.stride, wave_first, lane, &slab[wv][0]);
+    uint32_t acc = 0;
+    if (nlines) ls.issue(0);
+    for (uint64_t L = 0; L < nlines; ++L) {
+        uint32_t w[32];
+        ls.take(w, w + 16);
+        if (L + 1 < nlines) ls.issue(L + 1);
+#pragma unroll
+        for (int k = 0; k < 32; k += 2) acc = xor3(acc, w[k], w[k + 1]);
+    }
+    if (lane >= skip) gptr(sink)[wave_first + lane] = acc;
+}
+
+typedef unsigned int probe_v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void probe_linear_kernel(const probe_v4u* data, uint64_t n16, uint32_t* sink) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = tid;
+    for (; i + 3 * nth < n16; i += 4 * nth) {
+        probe_v4u v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(gptr(data) + i + k * nth);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = xor3(acc, xor3(v[k].x, v[k].y, v[k].z), v[k].w);
+    }
+    for (; i < n16; i += nth) {
+        const probe_v4u v = gptr(data)[i];
+        acc = xor3(acc, xor3(v.x, v.y, v.z), v.w);
+    }
+    gptr(sink)[tid] = acc;
+}
+
+void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s) {
+    if (mode == 0) {
+        hipLaunchKernelGGL(probe_records_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, s, a, sink);
+    } else {
+        const uint64_t n16 = a.count * a.stride / 16;
+        hipLaunchKernelGGL(probe_linear_kernel, dim3((unsigned)(8 * device_cu_count())), dim3(256), 0, s,
+                           reinterpret_cast<const probe_v4u*>(a.data), n16, sink);
+    }
+}
+
 // ---------------------------------------------------- length bucketing
 // Ragged batches: lanes of one wavefront run until the longest lane's message
 // is done, so a random mix of 64 B and 64 KiB messages would make almost

@@ -1,0 +1,65 @@
+"""HBM read probes (include/lcb_hash_gpu.h lcb_hash_gpu_read_probe): the
+bench's achievable-bandwidth numbers only count if the probes read every byte
+they claim to.  Records mode folds each record's whole 128-B lines into one
+word (XOR), linear mode folds its grid-stride share per thread; both are
+checked against numpy on the same bytes."""
+import errno
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.pyoracle import gen_stream
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import liblcb_amd
+    return liblcb_amd.lib()
+
+
+@pytest.mark.parametrize("count,stride,flen", [(64, 1024, 1024), (1000, 1024, 1024), (777, 1040, 1000),
+                                               (4096 + 5, 256, 200)])
+def test_records_probe_reads_every_line(L, count, stride, flen):
+    host = gen_stream(count + flen, count * stride)
+    data = torch.as_tensor(host, device="cuda")
+    sink = torch.zeros(count, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.lcb_hash_gpu_probe_sink_words(0, count) == count
+    assert L.lcb_hash_gpu_read_probe(0, data.data_ptr(), count, stride, flen, sink.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    nl = flen // 128
+    words = host.reshape(count, stride)[:, :nl * 128].copy().view(np.uint32).reshape(count, -1)
+    exp = np.bitwise_xor.reduce(words, axis=1) if nl else np.zeros(count, np.uint32)
+    assert np.array_equal(sink.cpu().numpy().view(np.uint32), exp)
+
+
+def test_linear_probe_reads_every_byte(L):
+    n = (3 << 20) + 48
+    host = gen_stream(11, n)
+    data = torch.as_tensor(host, device="cuda")
+    words = L.lcb_hash_gpu_probe_sink_words(1, 1)
+    assert words > 0
+    sink = torch.zeros(words, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.lcb_hash_gpu_read_probe(1, data.data_ptr(), n // 16, 16, 16, sink.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    got = np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32))
+    assert got == np.bitwise_xor.reduce(host.view(np.uint32))
+
+
+def test_probe_rejects_bad_shapes(L):
+    data = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    p, q = data.data_ptr(), sink.data_ptr()
+    assert L.lcb_hash_gpu_read_probe(0, p, 63, 1024, 1024, q, s) == errno.EINVAL     # < 64 records
+    assert L.lcb_hash_gpu_read_probe(0, p, 64, 1024, 100, q, s) == errno.EINVAL      # no whole line
+    assert L.lcb_hash_gpu_read_probe(0, p + 8, 64, 1024, 1024, q, s) == errno.EINVAL  # misaligned
+    assert L.lcb_hash_gpu_read_probe(1, p, 3, 5, 5, q, s) == errno.EINVAL            # not 16-B multiple
+    assert L.lcb_hash_gpu_read_probe(2, p, 64, 1024, 1024, q, s) == errno.EINVAL     # unknown mode
+    torch.cuda.synchronize()
