@@ -149,28 +149,33 @@ def hash_launch(alg, data, digests, count, stream, key=None):
 
 
 def time_alg(alg, data, digests, count, steps, warmup, world, key=None):
-    """Returns (wall seconds for `steps` passes, max over ranks; mean kernel ms)."""
+    """Returns (wall seconds for `steps` passes, max over ranks; mean kernel ms).
+
+    The kernel time is the HIP-event span of the timed region on the launch
+    stream divided by `steps` (back-to-back launches, so it is the average
+    launch duration plus the inter-kernel gap).  Events around every launch
+    add ~6 us per step on MI355X (tools/step_overhead.py), so only the two
+    ends are recorded."""
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for _ in range(warmup):
         check(hash_launch(alg, data, digests, count, sp, key))
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    e0.record(stream)
+    for _ in range(steps):
         check(hash_launch(alg, data, digests, count, sp, key))
-        e.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
-    kms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kms = e0.elapsed_time(e1) / steps
     return max_over_ranks(t, world), kms
 
 
