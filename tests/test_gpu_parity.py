@@ -185,6 +185,25 @@ def test_fixed_stride_partial_last_wave(gpu, oracle, count):
         assert np.array_equal(got, np.asarray(exp).view(np.uint32)), ("crc", count, stride, flen)
 
 
+def test_bit_length_high_word(gpu, oracle):
+    """A message of 512 MiB + 67 B: its bit length no longer fits 32 bits, so
+    the high word of MD5's LE length field (md5.h:282) and of SHA-512's
+    128-bit BE one (sha2.h:725-731) are exercised; the message starts
+    unaligned.  One lane walks 8M blocks (latency-bound, ~25 s per
+    algorithm), so this is the slowest GPU test."""
+    n = (1 << 29) + 67
+    data = gpu.gen_synthetic(0x4242, n + 5)
+    host = data.cpu().numpy()
+    offs, lens = np.array([5], np.uint64), np.array([n], np.uint32)
+    do, dl = dev(offs, np.int64), dev(lens, np.int32)
+    for alg in (1, 6):
+        exp = oracle.batch(alg, host, offs, lens)
+        got = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        assert np.array_equal(got, exp), alg
+    del data
+    torch.cuda.empty_cache()
+
+
 def test_unaligned_digest_output(gpu, oracle):
     data = gen_stream(1, 64 * 100)
     for alg in (1, 2, 6, 7):
