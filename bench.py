@@ -696,6 +696,18 @@ def main():
                 liblcb_amd.hash_batch(alg, arr, count=count, stride=MSG_LEN, fixed_len=MSG_LEN, out=hd)
                 best = min(best, time.perf_counter() - t0)
             e2e[kind + "_GiB_s"] = round(count * MSG_LEN / best / 2**30, 3)
+        # The link alone: one pinned 1 GiB host -> device copy (the ceiling of
+        # the pinned row above).
+        scratch = torch.empty_like(data)
+        best = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            scratch.copy_(host, non_blocking=True)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        e2e["h2d_copy_only_GiB_s"] = round(host.numel() / best / 2**30, 3)
+        del scratch
         e2e["path"] = "host buffer -> 64 MiB chunks, 2 streams, H2D -> kernel -> D2H digests"
         out["e2e"] = e2e
         torch.cuda.synchronize()
