@@ -815,12 +815,47 @@ struct GatherLineStream : LdsLineSlab {
     }
 };
 
-// Compresses `nfull` whole blocks starting at p; returns the pointer after them.
+// 128 message bytes as raw LE words (a0 = bytes 0..63, a1 = 64..127):
+// two 64-B blocks, or one 128-B block.
 template <class H>
+__device__ __forceinline__ void md_compress128(H& st, const uint32_t* a0, const uint32_t* a1) {
+    if constexpr (H::kBlock == 128) {
+        uint32_t w[32];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { w[k] = a0[k]; w[16 + k] = a1[k]; }
+        st.compress(w);
+    } else {
+        st.compress(a0);
+        st.compress(a1);
+    }
+}
+
+// Compresses `nfull` whole blocks starting at p; returns the pointer after them.
+// kPf: latency form for batches too small to fill the chip -- the loads of
+// the next 128 B are in flight while the current 128 B are compressed (two
+// register sets, fewer waves per SIMD); otherwise occupancy hides the load
+// latency and one set is kept.
+template <class H, bool kPf = false>
 __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p, uint64_t nfull) {
     uint32_t w[H::kWords];
     uint64_t b = 0;
-    if (H::kPairLoad) {  // two blocks = one 128-B line per iteration
+    if constexpr (kPf) {  // 128 B per stage: two 64-B blocks or one 128-B block
+        constexpr int kPer = 128 / H::kBlock;
+        const uint64_t nl = nfull / kPer;
+        uint32_t a0[16], a1[16], b0[16], b1[16];
+        if (nl) load_full128(p, a0, a1);
+        uint64_t L = 0;
+        for (; L + 2 <= nl; L += 2) {
+            load_full128(p + 128 * (L + 1), b0, b1);
+            md_compress128(st, a0, a1);
+            if (L + 2 < nl) load_full128(p + 128 * (L + 2), a0, a1);
+            md_compress128(st, b0, b1);
+        }
+        if (L < nl) md_compress128(st, a0, a1);
+        b = nl * kPer;
+        p += 128 * nl;
+    }
+    if (H::kPairLoad && !kPf) {  // two blocks = one 128-B line per iteration
         uint32_t w1[16];
         for (; b + 2 <= nfull; b += 2, p += 128) {
             load_full128(p, w, w1);
@@ -853,11 +888,11 @@ __device__ __forceinline__ void md_pad_tail(H& st, uint32_t* w, uint32_t rem, ui
     st.compress(w);
 }
 
-template <class H>
+template <class H, bool kPf = false>
 __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
     uint32_t w[H::kWords];
     const uint64_t nfull = len / H::kBlock;
-    const uint8_t* p = md_full_blocks(st, msg, nfull);
+    const uint8_t* p = md_full_blocks<H, kPf>(st, msg, nfull);
     const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
     load_block_tail<H>(p, rem, w);
     md_pad_tail(st, w, rem, len + prefix);

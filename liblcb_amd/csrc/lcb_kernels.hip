@@ -23,19 +23,25 @@ __device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint
 // ------------------------------------------------------------- MD family
 // Message body: fixed-length batches of whole blocks take the pad-only final
 // block from the kernel-argument length (wave-uniform, scalar schedule).
-template <class H>
+template <class H, bool kPf>
 __device__ __forceinline__ void md_body(H& st, const KArgs& a, const uint8_t* msg, uint64_t len,
                                         uint64_t prefix) {
     if (!a.lengths && a.fixed_len % H::kBlock == 0) {
-        md_full_blocks(st, msg, (uint64_t)a.fixed_len / H::kBlock);
+        md_full_blocks<H, kPf>(st, msg, (uint64_t)a.fixed_len / H::kBlock);
         md_pad_only(st, (uint64_t)a.fixed_len + prefix);
     } else {
-        md_message(st, msg, len, prefix);
+        md_message<H, kPf>(st, msg, len, prefix);
     }
 }
 
-template <class H, bool kHmac>
-__global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
+// kPf: small batches (fewer than kPfMaxCount messages: at most one wave per
+// SIMD, so occupancy cannot hide the load latency) take the prefetching
+// message loop with the whole register file available (two 128-B stages
+// stay in VGPRs); otherwise the occupancy-bound loop at H::kOcc waves per
+// SIMD.
+constexpr uint64_t kPfMaxCount = 16384;
+template <class H, bool kHmac, bool kPf = false>
+__global__ __launch_bounds__(256, kPf ? 1 : H::kOcc) void md_batch_kernel(KArgs a) {
     uint64_t idx, len;
     const uint8_t* msg;
     if (!msg_at(a, idx, msg, len)) return;
@@ -43,7 +49,7 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
     uint32_t dw[H::kDigest / 4];
     if (kHmac) {
         load_words(st.s, a.mid);                       // state after K ^ ipad
-        md_body(st, a, msg, len, (uint64_t)H::kBlock);
+        md_body<H, kPf>(st, a, msg, len, (uint64_t)H::kBlock);
         st.digest_words(dw);
         H o;
         load_words(o.s, a.mid + kMidWords);            // state after K ^ opad
@@ -51,7 +57,7 @@ __global__ __launch_bounds__(256, H::kOcc) void md_batch_kernel(KArgs a) {
         o.digest_words(dw);
     } else {
         st.init();
-        md_body(st, a, msg, len, 0);
+        md_body<H, kPf>(st, a, msg, len, 0);
         st.digest_words(dw);
     }
     store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
@@ -778,6 +784,11 @@ static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
                                (uint32_t)(grid * kTileStreamWaves), (uint32_t)(grid * kTileWaves));
             return;
         }
+    }
+    if (a.count < kPfMaxCount) {
+        if (hmac) hipLaunchKernelGGL((md_batch_kernel<H, true, true>), grid_for(a.count), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((md_batch_kernel<H, false, true>), grid_for(a.count), dim3(256), 0, s, a);
+        return;
     }
     if (hmac) hipLaunchKernelGGL((md_batch_kernel<H, true>), grid_for(a.count), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((md_batch_kernel<H, false>), grid_for(a.count), dim3(256), 0, s, a);
