@@ -121,16 +121,16 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     // The bucketing permutation holds message indices as uint32.
     if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
-        // work: [kBucketKeys key cursors | 1 tile-queue head | count order]
-        const size_t bytes = (kBucketKeys + 1 + a.count) * sizeof(uint32_t);
+        // work: [key histogram | key fill counters | tile-queue head | count order]
+        const size_t bytes = (kBucketWork + a.count) * sizeof(uint32_t);
         if (work_buf) {
             work = work_buf;
         } else {
             LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&work), bytes, s));
         }
-        launch_bucketing(a, work, work + kBucketKeys + 1, s);
-        a.tile_next = work + kBucketKeys;
-        a.order = work + kBucketKeys + 1;
+        launch_bucketing(a, work, work + kBucketWork, s);
+        a.tile_next = work + kBucketHead;
+        a.order = work + kBucketWork;
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();

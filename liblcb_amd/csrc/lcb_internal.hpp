@@ -58,6 +58,10 @@ struct KeyBlock {
 // Bucket keys of ragged-batch bucketing (see lcb_kernels.hip): a length
 // class (< 128) and the record's 64-B half-line phase, key = class * 2 + half.
 constexpr int kBucketKeys = 256;
+// Bucketing scratch ahead of the permutation: key histogram, per-key fill
+// counters, the tile-queue head (uint32 words).
+constexpr int kBucketHead = 2 * kBucketKeys;
+constexpr int kBucketWork = 2 * kBucketKeys + 1;
 // Ragged batches at least this large are bucketed by length first.
 constexpr uint64_t kBucketMinCount = 4096;
 
@@ -95,7 +99,8 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
 void launch_crc(int variant, const KArgs& a, hipStream_t s);
 void crc_table_host(int variant, uint32_t* out);
 // Bucketing permutation of the ragged batch `a` (reads data/offsets/stride/
-// lengths/count) into `order`; `work` = kBucketKeys cursors + the tile-queue head.
+// lengths/count) into `order`; `work` = kBucketWork words (histogram, fill
+// counters, tile-queue head), zeroed here.
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream_t s);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
                       uint32_t* mid, hipStream_t s);
@@ -126,7 +131,7 @@ hipError_t scratch_free(void* p, hipStream_t s);
 int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
                uint8_t** dkey_out);
 // Batch kernel launch, bucketing a large ragged batch by length first.
-// work_buf: optional caller-owned device buffer of (kBucketKeys + 1 + count)
+// work_buf: optional caller-owned device buffer of (kBucketWork + count)
 // uint32 for the bucketing of a ragged batch; null = stream-ordered allocation.
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf = nullptr);
 

@@ -699,7 +699,13 @@ __device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
     return (len_class(gptr(a.lengths)[i]) << 1) | half;
 }
 
-__global__ __launch_bounds__(256) void bucket_hist_kernel(KArgs a, uint32_t* hist) {
+// Few, large blocks (kBucketBlocks x 1024 threads): every block adds its LDS
+// histogram to the global one with one atomic per key it saw, and the
+// atomics on a hot key serialise (one word takes ~88 per us,
+// MI355X_MICROARCH.md): 4096 blocks of 256 cost ~50 us on a 3-length batch.
+constexpr uint32_t kBucketBlocks = 512;
+
+__global__ __launch_bounds__(1024) void bucket_hist_kernel(KArgs a, uint32_t* hist) {
     __shared__ uint32_t h[kBucketKeys];
     for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
@@ -711,47 +717,49 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(KArgs a, uint32_t* his
         if (h[c]) atomicAdd(&hist[c], h[c]);
 }
 
-// Exclusive prefix over keys in DESCENDING key order -> start cursor.
-__global__ void bucket_scan_kernel(uint32_t* hist_to_cursor) {
-    if (threadIdx.x != 0) return;
-    uint32_t run = 0;
-    for (int c = kBucketKeys - 1; c >= 0; --c) {
-        const uint32_t n = hist_to_cursor[c];
-        hist_to_cursor[c] = run;
-        run += n;
-    }
-}
-
-// Each block reserves a contiguous range per key with one global atomic,
-// then scatters its indices (LDS atomics give the in-block rank).
-__global__ __launch_bounds__(256) void bucket_scatter_kernel(KArgs a, uint32_t* cursor, uint32_t* order) {
+// Block b owns the contiguous chunk [b * chunk, (b + 1) * chunk): it counts
+// its keys, reserves one range per key (start of the key in DESCENDING key
+// order, from the global histogram, + a per-key fill counter), then places
+// its indices (LDS atomics give the rank inside the block's range).
+__global__ __launch_bounds__(1024) void bucket_scatter_kernel(KArgs a, const uint32_t* hist, uint32_t* fill,
+                                                             uint32_t* order, uint64_t chunk) {
     __shared__ uint32_t h[kBucketKeys];
     __shared__ uint32_t base[kBucketKeys];
     for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t c = 0, r = 0;
-    if (i < a.count) {
-        c = bucket_key(a, i);
-        r = atomicAdd(&h[c], 1u);
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&h[bucket_key(a, i)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int c = kBucketKeys - 1; c >= 0; --c) {
+            base[c] = run;
+            run += hist[c];
+        }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < kBucketKeys; k += blockDim.x)
-        base[k] = h[k] ? atomicAdd(&cursor[k], h[k]) : 0u;
+    for (int k = threadIdx.x; k < kBucketKeys; k += blockDim.x) {
+        if (h[k]) base[k] += atomicAdd(&fill[k], h[k]);
+        h[k] = 0;
+    }
     __syncthreads();
-    if (i < a.count) order[base[c] + r] = (uint32_t)i;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t k = bucket_key(a, i);
+        order[base[k] + atomicAdd(&h[k], 1u)] = (uint32_t)i;
+    }
 }
 
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream_t s) {
-    // work: kBucketKeys key cursors + the tile-queue head, zeroed here;
-    // order: count uint32.
-    (void)hipMemsetAsync(work, 0, (kBucketKeys + 1) * sizeof(uint32_t), s);
-    uint64_t hb = (a.count + 255) / 256;
-    if (hb > 2048) hb = 2048;
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)hb), dim3(256), 0, s, a, work);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(64), 0, s, work);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, s, a, work,
-                       order);
+    // work: histogram | fill counters | tile-queue head, zeroed here; order:
+    // count uint32.
+    (void)hipMemsetAsync(work, 0, kBucketWork * sizeof(uint32_t), s);
+    uint64_t nb = (a.count + 1023) / 1024;
+    if (nb > kBucketBlocks) nb = kBucketBlocks;
+    const uint64_t chunk = (a.count + nb - 1) / nb;
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a, work);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((a.count + chunk - 1) / chunk)), dim3(1024), 0, s, a,
+                       work, work + kBucketKeys, order, chunk);
 }
 
 // ------------------------------------------------------------- launchers
