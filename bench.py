@@ -304,14 +304,17 @@ def cpu_baseline(alg, count, threads):
         res["port"] = (count * MSG_LEN / t / 2**30, t, d, 1)
     best = max(res, key=lambda k: res[k][0])
     path = {"reference": REF_SO, "reference-simd": REF_SIMD_SO}.get(best)
-    one = t16 = None
+    one = t16 = taff = None
     if path:
         r = Ref(path)
         n1 = min(count, 1 << 18)
         one = _ref_rate(r, alg, data, n1, 1, 0.0)[0]               # one pass, one thread
         if threads != 16:
             t16 = _ref_rate(r, alg, data, count, 16, 0.5)[0]       # the box's nominal CPU share
-    return best, res, one, t16, data
+        if affinity_cpus() != threads:
+            # every CPU of the affinity mask, whatever the quota allows
+            taff = _ref_rate(r, alg, data, count, affinity_cpus(), 0.5)[0]
+    return best, res, one, t16, taff, data
 
 
 def cpu_per_alg(data, threads, best):
@@ -716,7 +719,7 @@ def main():
 
     if rank == 0 and world == 1 and not a.no_cpu:
         threads = a.cpu_threads or host_threads()
-        best, res, one, t16, cdata = cpu_baseline(alg, count, threads)
+        best, res, one, t16, taff, cdata = cpu_baseline(alg, count, threads)
         gbs, tcpu, dcpu, reps = res[best]
         gpu_dig = digests[:count].cpu().numpy()
         out["cpu_baseline"] = {
@@ -729,6 +732,7 @@ def main():
             "all": {k: round(v[0], 3) for k, v in res.items()},
             "one_thread": round(one, 3) if one else None,
             "at_16_threads": round(t16, 3) if t16 else None,
+            "at_affinity_threads": round(taff, 3) if taff else None,
             "cgroup_cpus": cgroup_cpus(),
             "cpu_model": cpu_model(),
             "build_flags": {"reference": "gcc -O2 -fPIC, #undef __SSE2__ (as tests/hash/main.c:36)",
