@@ -747,6 +747,7 @@ struct LdsStridedStream : LdsLineSlab {
             voff[p] = (ln >> 3) * (uint32_t)stride + ((ln & 7) ^ f) * 16;
         }
     }
+    template <int kAux = kLdsAux>
     __device__ __forceinline__ void issue(uint64_t L) {
         // Offsets re-defined in place (no copy): zero-extended at each use, so
         // every DMA takes the saddr + 32-bit vaddr form.
@@ -760,7 +761,7 @@ struct LdsStridedStream : LdsLineSlab {
             const uint8_t* sb = wbase + so;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g & 1]),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
-                                             kLdsAux);
+                                             kAux);
         }
     }
 };

@@ -74,7 +74,11 @@ __global__ __launch_bounds__(256, kPf ? 1 : H::kOcc) void md_batch_kernel(KArgs 
 // half-line stages and taking the next line mid-way through the current one
 // (two line registers sets: 4 waves/SIMD) measured slower
 // (profiles/r1_lds_depth_ab.txt, r1_lds_half_ab.txt, r2_fixed_stream_ab.txt).
-template <class H, bool kHmac>
+// kAux: cache policy of the line stream -- nt when every record starts on a
+// 128-B line (each streamed line is one cache line, read once); default
+// otherwise, so the second cache line of a straddling 128-B line is still
+// in L2 when the record's next line asks for it.
+template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
     const uint32_t lane = threadIdx.x & 63;
@@ -97,11 +101,11 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     } else {
         st.init();
     }
-    if (nlines) ls.issue(0);
+    if (nlines) ls.issue<kAux>(0);
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
         ls.take(w, w + 16);                 // line L -> VGPRs, its buffer free again
-        if (L + 1 < nlines) ls.issue(L + 1);
+        if (L + 1 < nlines) ls.issue<kAux>(L + 1);
         if constexpr (H::kBlock == 128) {
             st.compress(w);                 // one SHA-384/512 block per line
         } else {
@@ -772,8 +776,13 @@ static void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
         // whole 128-B line.
         if (fixed_stride_lines(a)) {
             const dim3 grid((unsigned)((a.count + 255) / 256));
-            if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true>), grid, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false>), grid, dim3(256), 0, s, a);
+            if (a.stride % 128 == 0 && reinterpret_cast<uintptr_t>(a.data) % 128 == 0) {
+                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kLdsAux>), grid, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kLdsAux>), grid, dim3(256), 0, s, a);
+            } else {
+                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kGatherAux>), grid, dim3(256), 0, s, a);
+                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kGatherAux>), grid, dim3(256), 0, s, a);
+            }
             return;
         }
     }
