@@ -32,7 +32,9 @@ __global__ __launch_bounds__(256) void crc_batch_kernel(KArgs a) {
 // Fixed-stride batches (lcb_internal.hpp fixed_stride_lines): the 128-B lines
 // arrive through the per-wave LDS-DMA line stream (LdsStridedStream,
 // hash_device.hpp), line L+1 in flight while line L is folded in.
-template <int V>
+// kAux: the line stream's cache policy, chosen by alignment as for the digest
+// kernels (md_fixed_lds_kernel).
+template <int V, int kAux>
 __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     using Var = CrcVar<V>;
     __shared__ uint32_t T[8 * 256];
@@ -53,11 +55,11 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     const uint32_t c = a.init ? gptr(a.init)[i] : Var::kOneshot;
     const CrcRule<Var::kRefl> R{T};
     uint32_t r = Var::kInv ? ~c : c;
-    if (nlines) ls.issue(0);
+    if (nlines) ls.issue<kAux>(0);
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w0[16], w1[16];
         ls.take(w0, w1);
-        if (L + 1 < nlines) ls.issue(L + 1);
+        if (L + 1 < nlines) ls.issue<kAux>(L + 1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) r = R.step8(r, w0[2 * j], w0[2 * j + 1]);
 #pragma unroll
@@ -71,10 +73,12 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
 template <int V>
 static void launch_crc_v(const KArgs& a, hipStream_t s) {
     const uint64_t blocks = (a.count + 255) / 256;
-    if (fixed_stride_lines(a))
-        hipLaunchKernelGGL(crc_fixed_lds_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    else
+    if (!fixed_stride_lines(a))
         hipLaunchKernelGGL(crc_batch_kernel<V>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else if (a.stride % 128 == 0 && reinterpret_cast<uintptr_t>(a.data) % 128 == 0)
+        hipLaunchKernelGGL((crc_fixed_lds_kernel<V, kLdsAux>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((crc_fixed_lds_kernel<V, kGatherAux>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
 void launch_crc(int variant, const KArgs& a, hipStream_t s) {
