@@ -444,6 +444,83 @@ def bench_c4(alg, warmup, steps, count=MSGS_PER_GPU):
     return res
 
 
+def _event_ms(launch, warmup, steps, stream):
+    """Mean HIP-event span per launch over `steps` back-to-back launches on
+    `stream` (events at the two ends only), after `warmup` launches."""
+    for _ in range(warmup):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def bench_packets(warmup, steps, algs=("md5",)):
+    """The network-packet shape of the reference's caller (SURVEY.md 8(f) row 1,
+    VERDICT r2 item 1): 1M RADIUS-sized packets, lengths uniform 20..4096 B
+    (include/proto/radius.h:576), packed back to back at byte offsets as in a
+    receive buffer (src/threadpool/threadpool_task.c:692-696); device
+    resident, ragged batch bucketed by length on the device (counted in the
+    time).  Rows: plain digest, HMAC (one key), and keyed batches with 64
+    peer secrets (src/proto/radius_client.c:242,885,1025): HMAC
+    (Message-Authenticator, radius.h:850-919) and H(m || K) (packet
+    authenticator, radius.h:1315-1377); each checked against the reference's
+    digest-of-digests (tests/golden/packets.json).  Algorithmic bytes = packet
+    bytes + per packet (digest + 8 B offset + 4 B length [+ 4 B key index])."""
+    from tests.golden_util import packet_key_index, packet_keys, packet_layout
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "packets.json")))
+    offs, lens, total = packet_layout()
+    count = len(lens)
+    data = liblcb_amd.gen_synthetic(SEED, total)
+    d_offs = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    d_lens = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    d_kidx = torch.as_tensor(packet_key_index().astype(np.int32), device="cuda")
+    keys = [bytes(k) for k in packet_keys()]
+    blob = np.frombuffer(b"".join(keys), np.uint8)
+    klen = np.array([len(k) for k in keys], np.uint32)
+    koff = np.zeros(len(keys), np.uint64)
+    koff[1:] = np.cumsum(klen[:-1], dtype=np.uint64)
+    hkey = bytes.fromhex(fx["hmac_key_hex"])
+    stream = torch.cuda.current_stream()
+    res = {"packets": count, "total_GiB": round(total / 2**30, 4), "lengths": "uniform 20..4096 B",
+           "layout": "packed at byte offsets (%d of 16 alignments)" % len(np.unique(offs % 16)),
+           "keys": len(keys), "bucketed": True}
+    for alg_name in algs:
+        alg = ALG_IDS[alg_name]
+        D = DIGEST_SIZE[alg]
+        dig = torch.empty((count, D), dtype=torch.uint8, device="cuda")
+        rows = [("plain", None, None), ("hmac", hkey, None), ("keyed_hmac", None, 1), ("keyed_suffix", None, 3)]
+        for kind, key, mode in rows:
+            if mode and "keyed_%s_%s" % ({1: "hmac", 3: "suffix"}[mode], alg_name) not in fx["full"]:
+                continue
+
+            def launch():
+                if mode:
+                    check(lib().lcb_hash_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data,
+                                                     klen.ctypes.data, len(keys), d_kidx.data_ptr(),
+                                                     data.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                                     count, 0, 0, dig.data_ptr(), F_DEVICE, stream.cuda_stream))
+                else:
+                    check(lib().lcb_hash_batch(alg, key, len(key) if key else 0, data.data_ptr(),
+                                               d_offs.data_ptr(), d_lens.data_ptr(), count, 0, 0,
+                                               dig.data_ptr(), F_DEVICE, stream.cuda_stream))
+            ms = _event_ms(launch, warmup, steps, stream)
+            ab = total + count * (D + 12 + (4 if mode else 0))
+            name = "%s_%s" % (kind, alg_name)
+            ok = hashlib.sha256(dig.cpu().numpy().tobytes()).hexdigest() == fx["full"][name]["dod"]
+            res[name] = {"GiB_s": round(total / (ms * 1e-3) / 2**30, 2), "ms_per_pass": round(ms, 4),
+                         "hbm_frac": round(ab / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "dod_equals_reference": ok}
+        del dig
+    del data, d_offs, d_lens, d_kidx
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_crc(data, count, steps):
     """CRC-32 family (include/math/crc32.h) over the same
     1M x 1 KiB device-resident bytes: per-variant kernel time (HIP events,
@@ -680,6 +757,7 @@ def main():
             del dg
         out["hmac"] = hm
         out["ragged_c4"] = bench_c4(alg, a.warmup, max(3, a.steps // 4))
+        out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4))
         out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
         settle()   # ChaCha20 is VALU-heavy: let the clock settle after the HBM-bound CRC launches
         out["chacha"] = bench_chacha(data, count, max(3, a.steps // 4))

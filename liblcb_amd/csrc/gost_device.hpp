@@ -186,22 +186,28 @@ using lds_u64 = __attribute__((address_space(3))) const uint64_t;
 
 struct GostRot : GostNaturalOrder {
     lds_u8* L;
-    uint32_t off[8];     // (8c + ((j' + r) & 7)) * 8
-    uint32_t m1, m2, m4;  // all-ones where bit 0 / 1 / 2 of r is set
+    // Byte j & 3 of offp[j >> 2] = (8c + ((j' + r) & 7)) * 8 (< 256): the lane's
+    // bank-pair offsets for the 8 steps, packed 4 to a VGPR (v_perm picks the
+    // byte), 6 VGPRs fewer than one per step.
+    uint32_t offp[2];
+    // Bits 0 / 1 / 2 of r as lane masks (SGPR pairs feeding v_cndmask, not
+    // three all-ones VGPRs).
+    bool b1, b2, b4;
     __device__ __forceinline__ void init(lds_u8* lds) {
         L = lds;
         const uint32_t l = threadIdx.x & 31u, c = l >> 3, r = l & 7u;
+        offp[0] = offp[1] = 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) off[j] = (8u * c + (((uint32_t)j + r) & 7u)) * 8u;
-        m1 = (r & 1u) ? 0xffffffffu : 0u;
-        m2 = (r & 2u) ? 0xffffffffu : 0u;
-        m4 = (r & 4u) ? 0xffffffffu : 0u;
+        for (int j = 0; j < 8; ++j) offp[j >> 2] |= ((8u * c + (((uint32_t)j + r) & 7u)) * 8u) << (8 * (j & 3));
+        b1 = (r & 1u) != 0;
+        b2 = (r & 2u) != 0;
+        b4 = (r & 4u) != 0;
     }
     template <int S>
-    __device__ __forceinline__ static void rot(uint32_t (&v)[8], uint32_t m) {  // v[j] <- v[(j + S) & 7] where m
+    __device__ __forceinline__ static void rot(uint32_t (&v)[8], bool m) {  // v[j] <- v[(j + S) & 7] where m
         uint32_t t[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = ch3(m, v[(j + S) & 7], v[j]);
+        for (int j = 0; j < 8; ++j) t[j] = m ? v[(j + S) & 7] : v[j];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = t[j];
     }
@@ -210,17 +216,18 @@ struct GostRot : GostNaturalOrder {
         uint32_t lo[8], hi[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { lo[j] = (uint32_t)x[j]; hi[j] = (uint32_t)(x[j] >> 32); }
-        rot<1>(lo, m1); rot<1>(hi, m1);
-        rot<2>(lo, m2); rot<2>(hi, m2);
-        rot<4>(lo, m4); rot<4>(hi, m4);   // lo/hi[j'] = word (j' + r) & 7
+        rot<1>(lo, b1); rot<1>(hi, b1);
+        rot<2>(lo, b2); rot<2>(hi, b2);
+        rot<4>(lo, b4); rot<4>(hi, b4);   // lo/hi[j'] = word (j' + r) & 7
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            // address bytes: [0] = off (S1 byte 0), [1] = byte i&3 of the word (S0), [2,3] = 0
-            const uint32_t sel = 0x0c0c0000u | ((4u + (uint32_t)(i & 3)) << 8);
             uint64_t v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint32_t a = __builtin_amdgcn_perm((i < 4) ? lo[j] : hi[j], off[j], sel);
+                // address bytes: [0] = step j's offset (S1 byte j & 3), [1] = byte
+                // i & 3 of the word (S0), [2,3] = 0
+                const uint32_t sel = 0x0c0c0000u | ((4u + (uint32_t)(i & 3)) << 8) | (uint32_t)(j & 3);
+                const uint32_t a = __builtin_amdgcn_perm((i < 4) ? lo[j] : hi[j], offp[j >> 2], sel);
                 v[j] = *reinterpret_cast<lds_u64*>(L + a);
             }
             uint32_t l = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]),
@@ -230,6 +237,10 @@ struct GostRot : GostNaturalOrder {
                               xor3((uint32_t)(v[3] >> 32), (uint32_t)(v[4] >> 32), (uint32_t)(v[5] >> 32)),
                               (uint32_t)(v[6] >> 32) ^ (uint32_t)(v[7] >> 32));
             o[i] = ((uint64_t)h << 32) | l;
+            // Scheduling fence after every 4 output words: bounds the ds_read
+            // lookahead, which otherwise grows until the 128-VGPR budget of the
+            // 4-waves-per-SIMD kernels spills (kernel_resources test).
+            if ((i + 1) % 4 == 0) __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
@@ -246,60 +257,94 @@ __device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
 // the hooks let tools/gost_half.hpp's lane-ordered layout run the same code).
 template <class Tab>
 __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
+    // E(K, m) as 12 (K, t) steps plus the last key, from K_0 = h, t_0 = m:
+    //   step r: K_{r+1} = LPS(K_r ^ c_r), t_{r+1} = LPS(t_r ^ K_{r+1}),
+    //   c_0 = N, c_r = C_{r-1};  K_13 = LPS(K_12 ^ C_11) (step 12, no t).
+    // One rolled loop: two LPS bodies per kernel instead of five, so every
+    // g in a kernel shares one register allocation.
     uint64_t k[8], t[8], x[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = h[i];
-    T.xor_n(x, n0);
-    T.lps(k, x);                                         // K = LPS(h ^ N)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = k[i] ^ m[i];
-    T.lps(t, x);                                         // t = LPS(K ^ m)
-    // Rounds 1..11: K = LPS(K ^ C_{r-1}); t = LPS(t ^ K).  Kept rolled: the
-    // body is 128 LDS lookups already.  (Issuing t_r and K_{r+1} together --
-    // both need only K_r -- measured the same: tools/gost_lanes_ab.hip.)
+    for (int i = 0; i < 8; ++i) {
+        k[i] = h[i];
+        t[i] = m[i];
+        h[i] ^= m[i];   // the feed-forward h ^ m of :1142, taken now: m and the old h die here
+    }
 #pragma unroll 1
-    for (int r = 0; r < 11; ++r) {
-        T.xor_c(x, k, r);
-        T.lps(k, x);                                     // K = LPS(K ^ C_r)
+    for (int r = 0; r < 13; ++r) {
+        if (r == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = k[i];
+            T.xor_n(x, n0);
+        } else {
+            T.xor_c(x, k, r - 1);
+        }
+        T.lps(k, x);                                     // K_{r+1} = LPS(K_r ^ c_r)
+        if (r == 12) break;
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = t[i] ^ k[i];
-        T.lps(t, x);                                     // t = LPS(t ^ K)
+        T.lps(t, x);                                     // t_{r+1} = LPS(t_r ^ K_{r+1})
     }
-    T.xor_c(x, k, 11);
-    T.lps(k, x);                                         // K13 = LPS(K ^ C_11)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] ^= m[i] ^ t[i] ^ k[i];  // :1142
+    for (int i = 0; i < 8; ++i) h[i] ^= t[i] ^ k[i];     // :1142 (h already holds h ^ m)
 }
 
 // The chaining value h is kept in the table's lane order between blocks
 // (natural for the product's tables); Sigma and N in natural order.  The IV (all words equal) reads the
 // same in every order.
-template <bool k256>
+//
+// kSgStride > 0: Sigma lives in LDS (word i of thread x at
+// sgl_base[i * kSgStride + x], bind_sigma), not in VGPRs.  Sigma is touched
+// once per block, and its 16 VGPRs are what pushed the batch kernels (4 waves
+// per SIMD, 128 VGPRs) into scratch spills.
+using lds_u64w = __attribute__((address_space(3))) uint64_t;
+template <bool k256, int kSgStride = 0>
 struct Gost {
     static constexpr int kBlock = 64, kDigest = k256 ? 32 : 64, kWords = 16;
-    uint64_t h[8], n0, sg[8];
+    uint64_t h[8], n0, sg[kSgStride ? 1 : 8];
+    lds_u64w* sgl;   // kSgStride: this thread's Sigma words (stride kSgStride)
+    __device__ __forceinline__ void bind_sigma(lds_u64w* base) {
+        if constexpr (kSgStride) sgl = base + threadIdx.x;
+    }
+    __device__ __forceinline__ uint64_t sigma(int i) const {
+        if constexpr (kSgStride) return sgl[i * kSgStride];
+        else return sg[i];
+    }
+    // Sigma for the final g_0(h, Sigma), read back from LDS (volatile): else
+    // the compiler forwards the words just stored and keeps them in VGPRs
+    // through g_0(h, N), which spilled.
+    __device__ __forceinline__ uint64_t sigma_final(int i) const {
+        if constexpr (kSgStride) return *(volatile lds_u64w*)&sgl[i * kSgStride];
+        else return sg[i];
+    }
+    __device__ __forceinline__ void set_sigma(int i, uint64_t v) {
+        if constexpr (kSgStride) sgl[i * kSgStride] = v;
+        else sg[i] = v;
+    }
     __device__ __forceinline__ void init() {  // gost3411-2012.h:1713-1729
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { h[i] = k256 ? 0x0101010101010101ull : 0ull; sg[i] = 0; }
+        for (int i = 0; i < 8; ++i) { h[i] = k256 ? 0x0101010101010101ull : 0ull; set_sigma(i, 0); }
         n0 = 0;
     }
     // One g_N step over raw LE words w (gost3411-2012.h:1129-1131).
+    // Sigma += m mod 2^512 (gost3411-2012.h:996-1013).
+    __device__ __forceinline__ void add_sigma(const uint64_t m[8]) {
+        uint32_t carry = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t s1 = sigma(i) + m[i];
+            const uint32_t c1 = s1 < m[i];
+            const uint64_t s2 = s1 + carry;
+            carry = c1 | (s2 < s1);
+            set_sigma(i, s2);
+        }
+    }
     template <class Tab>
     __device__ __forceinline__ void block(const uint32_t* w, uint64_t bits, const Tab& T) {
         uint64_t m[8], ml[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
-        // Sigma += m mod 2^512 (gost3411-2012.h:996-1013), before g_N so
-        // that only the lane-ordered copy of m stays live through it.
-        uint32_t carry = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint64_t s1 = sg[i] + m[i];
-            const uint32_t c1 = s1 < m[i];
-            const uint64_t s2 = s1 + carry;
-            carry = c1 | (s2 < s1);
-            sg[i] = s2;
-        }
+        // Sigma first, so that only the lane-ordered copy of m stays live through g_N.
+        add_sigma(m);
         T.to_lane(ml, m);
         gost_g(h, n0, ml, T);
         n0 += bits;
@@ -315,7 +360,9 @@ struct Gost {
         for (int i = 1; i < 8; ++i) m[i] = 0;
         T.to_lane(ml, m);
         gost_g(h, 0, ml, T);   // g_0(h, N)
-        T.to_lane(ml, sg);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = sigma_final(i);
+        T.to_lane(ml, m);
         gost_g(h, 0, ml, T);   // g_0(h, Sigma)
     }
     template <class Tab>
@@ -336,7 +383,7 @@ struct Gost {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             p[2 * i] = (uint32_t)hn[i]; p[2 * i + 1] = (uint32_t)(hn[i] >> 32);
-            p[18 + 2 * i] = (uint32_t)sg[i]; p[19 + 2 * i] = (uint32_t)(sg[i] >> 32);
+            p[18 + 2 * i] = (uint32_t)sigma(i); p[19 + 2 * i] = (uint32_t)(sigma(i) >> 32);
         }
         p[16] = (uint32_t)n0; p[17] = (uint32_t)(n0 >> 32);
     }
@@ -346,52 +393,80 @@ struct Gost {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             hn[i] = (uint64_t)p[2 * i] | ((uint64_t)p[2 * i + 1] << 32);
-            sg[i] = (uint64_t)p[18 + 2 * i] | ((uint64_t)p[19 + 2 * i] << 32);
+            set_sigma(i, (uint64_t)p[18 + 2 * i] | ((uint64_t)p[19 + 2 * i] << 32));
         }
         T.to_lane(h, hn);
         n0 = (uint64_t)p[16] | ((uint64_t)p[17] << 32);
     }
 };
 
-// Whole message through a GOST state (gost3411_2012_update + _final).
-template <bool k256, class Tab>
-__device__ __forceinline__ void gost_message(Gost<k256>& st, const uint8_t* msg, uint64_t len, const Tab& T) {
+// Message sources of gost_run: whole 64-B block j (j < nfull) and the
+// zero-filled tail of r = rem() < 64 bytes (tail_n), as raw LE words.
+struct GostPlainSrc {   // msg[0, len)
+    const uint8_t* p;
+    uint64_t len;
+    __device__ __forceinline__ uint64_t nfull() const { return len >> 6; }
+    __device__ __forceinline__ uint32_t rem() const { return (uint32_t)(len & 63u); }
+    __device__ __forceinline__ void block(uint64_t j, uint32_t w[16]) const { load_full64(p + 64 * j, w); }
+    __device__ __forceinline__ void tail_n(uint32_t w[16], uint32_t r) const { load_tail64(p + (len & ~63ull), r, w); }
+};
+struct GostVirtSrc {    // A[0, la) || B[0, lb) (keyed batches), nothing copied
+    const uint8_t* A;
+    uint64_t la;
+    const uint8_t* B;
+    uint64_t lb;
+    __device__ __forceinline__ uint64_t nfull() const { return (la + lb) >> 6; }
+    __device__ __forceinline__ uint32_t rem() const { return (uint32_t)((la + lb) & 63u); }
+    __device__ __forceinline__ void block(uint64_t j, uint32_t w[16]) const {
+        const uint64_t pos = 64 * j;
+        if (pos + 64 <= la) load_full64(A + pos, w);
+        else if (pos >= la) load_full64(B + (pos - la), w);
+        else load_vblock64(A, la, B, lb, pos, w);     // the seam block
+    }
+    __device__ __forceinline__ void tail_n(uint32_t w[16], uint32_t r) const {   // r == rem()
+        const uint64_t pos = (la + lb) & ~63ull;
+        if (pos >= la) load_tail64(B + (pos - la), r, w);
+        else load_vblock64(A, la, B, lb, pos, w);     // zero fill past la + lb
+    }
+};
+
+// One whole message through a GOST state (gost3411_2012_update + _final,
+// gost3411-2012.h:1743-1843): the whole blocks, then the tail || 0x01 and the
+// two g_0 steps (Gost::finish).
+template <class G, class Src, class Tab>
+__device__ __forceinline__ void gost_run(G& st, const Src& src, const Tab& T) {
     uint32_t w[16];
-    const uint64_t nfull = len / 64;
-    const uint8_t* p = msg;
-    for (uint64_t b = 0; b < nfull; ++b, p += 64) {
-        load_full64(p, w);
+    const uint64_t nfull = src.nfull();
+    for (uint64_t j = 0; j < nfull; ++j) {
+        src.block(j, w);
         st.block(w, 512, T);
     }
-    const uint32_t rem = (uint32_t)(len - nfull * 64);
-    load_tail64(p, rem, w);
+    const uint32_t rem = src.rem();
+    src.tail_n(w, rem);
     st.finish(w, rem, T);
 }
 
-// Virtual message A[0, la) || B[0, lb) (keyed batches): as gost_message,
-// the seam block assembled from both.
-template <bool k256, class Tab>
-__device__ __forceinline__ void gost_message2(Gost<k256>& st, const uint8_t* A, uint64_t la, const uint8_t* B,
-                                              uint64_t lb, const Tab& T) {
+// HMAC outer pass (gost3411-2012.h:1902-1934): the D-byte inner digest dw
+// hashed from the state after K ^ opad (mid_outer).
+template <class G, class Tab>
+__device__ __forceinline__ void gost_outer(G& o, const uint32_t* dw, const uint32_t* mid_outer, const Tab& T) {
+    o.load(mid_outer, T);
     uint32_t w[16];
-    const uint64_t nA = la / 64;
-    for (uint64_t b = 0; b < nA; ++b) {
-        load_full64(A + 64 * b, w);
-        st.block(w, 512, T);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
+    if (G::kDigest == 64) {       // a 64-byte digest is a full block, then an
+        o.block(w, 512, T);       // empty pad block (gost3411-2012.h:1783-1793)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = 0u;
+        o.finish(w, 0, T);
+    } else {
+        o.finish(w, G::kDigest, T);  // 32 bytes: the digest is the tail block
     }
-    uint64_t done = nA * 64;
-    const uint64_t total = la + lb;
-    while (done < la && done + 64 <= total) {
-        load_vblock64(A, la, B, lb, done, w);
-        st.block(w, 512, T);
-        done += 64;
-    }
-    if (done >= la) {
-        gost_message(st, B + (done - la), total - done, T);
-        return;
-    }
-    load_vblock64(A, la, B, lb, done, w);
-    st.finish(w, (uint32_t)(total - done), T);
+}
+
+template <class G, class Tab>
+__device__ __forceinline__ void gost_message(G& st, const uint8_t* msg, uint64_t len, const Tab& T) {
+    gost_run(st, GostPlainSrc{msg, len}, T);
 }
 
 }  // namespace lcbgpu

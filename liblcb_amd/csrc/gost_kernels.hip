@@ -1,0 +1,226 @@
+// gost_kernels.hip — GOST R 34.11-2012 (Streebog) batch kernels and their
+// launchers (gost_device.hpp holds the per-lane transform).
+#include <hip/hip_runtime.h>
+#include "gost_device.hpp"
+#include "hash_device.hpp"
+#include "lcb_internal.hpp"
+
+namespace lcbgpu {
+
+__device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.count) return false;
+    idx = a.order ? (uint64_t)gptr(a.order)[i] : i;
+    msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
+    len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
+    return true;
+}
+
+__device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
+    const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
+    return k < a.nkeys ? k : a.nkeys - 1;   // out of range: the last key (documented)
+}
+
+// Message index of this lane, re-derived where the digest is stored (the
+// thread index passes through an empty asm, so the compiler reloads it
+// instead of keeping the 64-bit index live through the whole message: two
+// VGPRs of the 128 the GOST kernels may use).
+__device__ __forceinline__ uint64_t store_index(const KArgs& a) {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
+    return a.order ? (uint64_t)gptr(a.order)[i] : i;
+}
+
+// ------------------------------------------------------------------ GOST
+// One 1024-thread workgroup per CU (16 waves: four per SIMD, so at most 128
+// VGPRs per lane) sharing ONE 64 KiB rotated LPS image (gost_device.hpp
+// GostRot), and every lane's Sigma in the LDS beside it (64 KiB, Gost<k256,
+// kGostThreads>): 128 KiB of the CU's 160.  Round 2 ran two 512-thread
+// workgroups per CU, each with its own image and Sigma in VGPRs: at 128 VGPRs
+// that spilled 12-68 B per lane to scratch (1.45-1.58x the algorithmic HBM
+// traffic).  (Two 256-thread workgroups at up to 256 VGPRs were 2-3 %
+// slower; tools/gost_lanes_ab.hip)
+constexpr int kGostThreads = 1024;
+template <bool k256, bool kHmac>
+__global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
+    __shared__ __attribute__((aligned(16))) uint64_t Sg[8 * kGostThreads];  // Sigma of every lane
+    gost_stage_rot(Timg);
+    GostRot T;
+    T.init((lds_u8*)Timg);
+    uint64_t idx, len;
+    const uint8_t* msg;
+    if (!msg_at(a, idx, msg, len)) return;
+    using G = Gost<k256, kGostThreads>;
+    G st;
+    st.bind_sigma((lds_u64w*)Sg);
+    uint32_t dw[G::kDigest / 4];
+    if (kHmac) {
+        st.load(a.mid, T);   // state after K ^ ipad; the outer pass from K ^ opad
+        gost_run(st, GostPlainSrc{msg, len}, T);
+        st.digest_words(dw, T);
+        gost_outer(st, dw, a.mid + kMidWords, T);
+    } else {
+        st.init();
+        gost_run(st, GostPlainSrc{msg, len}, T);
+    }
+    st.digest_words(dw, T);
+    store_digest<G::kDigest>(a.digests + store_index(a) * G::kDigest, dw);
+}
+
+// Keyed GOST batches (see md_keyed_kernel).
+template <bool k256, int kMode>
+__global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];
+    __shared__ __attribute__((aligned(16))) uint64_t Sg[8 * kGostThreads];
+    gost_stage_rot(Timg);
+    GostRot T;
+    T.init((lds_u8*)Timg);
+    uint64_t idx, len;
+    const uint8_t* msg;
+    if (!msg_at(a, idx, msg, len)) return;
+    using G = Gost<k256, kGostThreads>;
+    const uint32_t k = key_of(a, idx);
+    const uint32_t* mid = gptr(a.mid) + (uint64_t)k * 2 * kMidWords;
+    const uint8_t* K = gptr(a.keys) + gptr(a.key_off)[k];
+    const uint64_t kl = gptr(a.key_len)[k];
+    G st;
+    st.bind_sigma((lds_u64w*)Sg);
+    uint32_t dw[G::kDigest / 4];
+    if (kMode == kKeyHmac) {
+        st.load(mid, T);
+        gost_run(st, GostPlainSrc{msg, len}, T);
+        st.digest_words(dw, T);
+        // The key's outer mid-state, looked up again (not kept live through the message).
+        const uint64_t i2 = store_index(a);
+        gost_outer(st, dw, gptr(a.mid) + (uint64_t)key_of(a, i2) * 2 * kMidWords + kMidWords, T);
+    } else if (kMode == kKeyPrefix) {
+        // State after K's whole blocks; the rest of K and the message as one
+        // virtual message (radius.h:774-789 copies the keyed context the same way).
+        const uint64_t full = kl / 64 * 64;
+        st.load(mid, T);
+        gost_run(st, GostVirtSrc{K + full, kl - full, msg, len}, T);
+    } else {
+        st.init();
+        gost_run(st, GostVirtSrc{msg, len, K, kl}, T);
+    }
+    st.digest_words(dw, T);
+    store_digest<G::kDigest>(a.digests + store_index(a) * G::kDigest, dw);
+}
+
+// One lane per key (flat table; the whole block stages it first).
+template <bool k256>
+__global__ __launch_bounds__(256) void gost_key_prep_kernel(KArgs a, uint32_t* mid) {
+    __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
+    gost_stage_table(Timg);
+    const GostFlat T{{}, Timg};
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.nkeys) return;
+    using G = Gost<k256>;
+    const uint8_t* K = gptr(a.keys) + gptr(a.key_off)[k];
+    const uint64_t kl = gptr(a.key_len)[k];
+    uint32_t* m = mid + k * 2 * kMidWords;
+    G st;
+    st.init();
+    uint32_t w[16];
+    if (a.key_mode == kKeyPrefix) {
+        for (uint64_t b = 0; b < kl / 64; ++b) {
+            load_full64(K + 64 * b, w);
+            st.block(w, 512, T);
+        }
+        st.save(m, T);
+        return;
+    }
+    if (kl > 64) {  // gost3411-2012.h:1873-1878: long key -> its digest
+        gost_message(st, K, kl, T);
+        uint32_t dw[G::kDigest / 4];
+        st.digest_words(dw, T);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
+    } else if (kl == 64) {
+        load_full64(K, w);
+    } else {
+        load_tail64(K, (uint32_t)kl, w);
+    }
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = w[i] ^ 0x36363636u;
+    st.init();
+    st.block(x, 512, T);
+    st.save(m, T);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = w[i] ^ 0x5c5c5c5cu;
+    st.init();
+    st.block(x, 512, T);
+    st.save(m + kMidWords, T);
+}
+
+template <bool k256>
+__global__ __launch_bounds__(256) void gost_hmac_prep_kernel(KeyBlock kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid) {
+    __shared__ __attribute__((aligned(16))) uint64_t Timg[8 * 256];
+    gost_stage_table(Timg);
+    const GostFlat T{{}, Timg};
+    if (threadIdx.x != 0) return;
+    using G = Gost<k256>;
+    uint32_t k[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = kb.w[i];
+    if (dkey) {  // gost3411-2012.h:1873-1878: long key -> its digest
+        G st;
+        st.init();
+        gost_message(st, dkey, key_len, T);
+        uint32_t dw[G::kDigest / 4];
+        st.digest_words(dw, T);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) k[i] = (i < G::kDigest / 4) ? dw[i] : 0u;
+    }
+    uint32_t w[16];
+    G st;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x36363636u;
+    st.init();
+    st.block(w, 512, T);
+    st.save(mid, T);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = k[i] ^ 0x5c5c5c5cu;
+    st.init();
+    st.block(w, 512, T);
+    st.save(mid + kMidWords, T);
+}
+
+template <bool k256>
+void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
+    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
+    if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), g, dim3(kGostThreads), 0, s, a);
+    else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), g, dim3(kGostThreads), 0, s, a);
+}
+template <bool k256>
+void launch_gost_keyed(const KArgs& a, hipStream_t s) {
+    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
+    switch (a.key_mode) {
+    case kKeyHmac: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyHmac>), g, dim3(kGostThreads), 0, s, a); break;
+    case kKeyPrefix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyPrefix>), g, dim3(kGostThreads), 0, s, a); break;
+    case kKeySuffix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeySuffix>), g, dim3(kGostThreads), 0, s, a); break;
+    }
+}
+
+#define LCB_GOST_FAMILY(k256, tag)                                                                   \
+    void launch_plain_##tag(const KArgs& a, bool hmac, hipStream_t s) { launch_gost<k256>(a, hmac, s); } \
+    void launch_keyed_##tag(const KArgs& a, hipStream_t s) { launch_gost_keyed<k256>(a, s); }        \
+    void launch_key_prep_##tag(const KArgs& a, uint32_t* mid, hipStream_t s) {                      \
+        hipLaunchKernelGGL(gost_key_prep_kernel<k256>, dim3((unsigned)((a.nkeys + 255) / 256)), dim3(256), 0, s, a, mid); \
+    }                                                                                                \
+    void launch_hmac_prep_##tag(const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid, \
+                                hipStream_t s) {                                                     \
+        hipLaunchKernelGGL(gost_hmac_prep_kernel<k256>, dim3(1), dim3(256), 0, s, kb, dkey, key_len, mid); \
+    }
+LCB_GOST_FAMILY(true, gost256)
+LCB_GOST_FAMILY(false, gost512)
+
+void gost_table_host(uint64_t* out) {
+    for (int j = 0; j < 8; ++j)
+        for (int b = 0; b < 256; ++b) out[j * 256 + b] = kGostAxHost.t[j][b];
+}
+
+}  // namespace lcbgpu

@@ -1,0 +1,7 @@
+// k_sha384.hip — SHA384 batch kernels (md_kernels.hpp), one translation unit per
+// algorithm so the library compiles in parallel.
+#include "md_kernels.hpp"
+
+namespace lcbgpu {
+LCB_MD_FAMILY(Sha512<true>, sha384)
+}  // namespace lcbgpu

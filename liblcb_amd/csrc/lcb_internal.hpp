@@ -92,6 +92,24 @@ struct ChaArgs {
 };
 
 void launch_batch(int alg, const KArgs& a, hipStream_t s);
+// Per-algorithm launchers, one translation unit each (k_<alg>.hip,
+// gost_kernels.hip); launch_batch / launch_key_prep / launch_hmac_prep
+// dispatch to them by alg id.
+#define LCB_DECLARE_FAMILY(tag)                                                                       \
+    void launch_plain_##tag(const KArgs& a, bool hmac, hipStream_t s);                               \
+    void launch_keyed_##tag(const KArgs& a, hipStream_t s);                                          \
+    void launch_key_prep_##tag(const KArgs& a, uint32_t* mid, hipStream_t s);                        \
+    void launch_hmac_prep_##tag(const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len, uint32_t* mid, \
+                                hipStream_t s);
+LCB_DECLARE_FAMILY(md5)
+LCB_DECLARE_FAMILY(sha1)
+LCB_DECLARE_FAMILY(sha224)
+LCB_DECLARE_FAMILY(sha256)
+LCB_DECLARE_FAMILY(sha384)
+LCB_DECLARE_FAMILY(sha512)
+LCB_DECLARE_FAMILY(gost256)
+LCB_DECLARE_FAMILY(gost512)
+#undef LCB_DECLARE_FAMILY
 // ChaCha: ragged scan (parts: (count+1023)/1024 words, blk_start: count+1),
 // xchacha subkey prep (subkeys: 8 words per buffer), then the block kernel.
 void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t* blk_start,

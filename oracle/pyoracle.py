@@ -66,6 +66,34 @@ class _Batch:
         assert rc == 0, rc
         return out
 
+    def batch_keyed(self, alg, mode, keys, data, key_index=None, offsets=None, lengths=None, count=None,
+                    stride=0, fixed_len=0):
+        """Keyed batch (or_batch_keyed / ref_batch_keyed): mode 1 HMAC, 2 H(K || m),
+        3 H(m || K); keys: list of bytes."""
+        blob = np.frombuffer(b"".join(keys) or b"\0", np.uint8)
+        klen = np.array([len(k) for k in keys], np.uint32)
+        koff = np.zeros(len(keys), np.uint64)
+        koff[1:] = np.cumsum(klen[:-1], dtype=np.uint64)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if key_index is not None:
+            key_index = np.ascontiguousarray(key_index, dtype=np.uint32)
+        if count is None:
+            count = len(lengths) if lengths is not None else len(offsets)
+        out = np.zeros((count, DSIZE[alg]), np.uint8)
+        rc = self.fn_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data, len(keys),
+                                     key_index.ctypes.data if key_index is not None else None, data.ctypes.data,
+                                     offsets.ctypes.data if offsets is not None else None,
+                                     lengths.ctypes.data if lengths is not None else None, count, stride,
+                                     fixed_len, out.ctypes.data)
+        assert rc == 0, rc
+        return out
+
     def batch_fixed_mt(self, alg, data, count, stride, fixed_len, key=None, threads=8):
         """Fixed-stride batch split into `threads` contiguous shards (ctypes
         releases the GIL, so the shards run in parallel)."""
@@ -88,6 +116,10 @@ class _Batch:
 _ARGS = [_c.c_int, _c.c_char_p, _c.c_size_t, _c.c_void_p, _c.c_void_p, _c.c_void_p,
          _c.c_size_t, _c.c_uint64, _c.c_uint32, _c.c_void_p]
 
+
+_KEYED_ARGS = [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+               _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+               _c.c_uint64, _c.c_uint32, _c.c_void_p]
 
 _CRC_ARGS = [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
              _c.c_uint64, _c.c_uint32, _c.c_void_p]
@@ -176,41 +208,14 @@ class Oracle(_Batch, _Crc, _Cha):
         self.fn_cha = self.lib.or_chacha_batch
         self.lib.or_crc32_batch.argtypes = _CRC_ARGS
         self.fn_crc = self.lib.or_crc32_batch
-        self.lib.or_batch_keyed.argtypes = [_c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
-                                            _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_size_t,
-                                            _c.c_uint64, _c.c_uint32, _c.c_void_p]
+        self.lib.or_batch_keyed.argtypes = _KEYED_ARGS
+        self.fn_keyed = self.lib.or_batch_keyed
         self.lib.or_crc32_table.restype = _c.c_uint32
         self.lib.or_crc32_table.argtypes = [_c.c_int, _c.c_int]
 
     def crc32_table(self, variant):
         return np.array([self.lib.or_crc32_table(variant, i) for i in range(256)], np.uint32)
 
-    def batch_keyed(self, alg, mode, keys, data, key_index=None, offsets=None, lengths=None, count=None,
-                    stride=0, fixed_len=0):
-        """or_batch_keyed: mode 1 HMAC, 2 H(K || m), 3 H(m || K); keys: list of bytes."""
-        blob = np.frombuffer(b"".join(keys) or b"\0", np.uint8)
-        klen = np.array([len(k) for k in keys], np.uint32)
-        koff = np.zeros(len(keys), np.uint64)
-        koff[1:] = np.cumsum(klen[:-1], dtype=np.uint64)
-        data = np.ascontiguousarray(data, dtype=np.uint8)
-        if data.size == 0:
-            data = np.zeros(1, np.uint8)
-        if offsets is not None:
-            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-        if lengths is not None:
-            lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
-        if key_index is not None:
-            key_index = np.ascontiguousarray(key_index, dtype=np.uint32)
-        if count is None:
-            count = len(lengths) if lengths is not None else len(offsets)
-        out = np.zeros((count, DSIZE[alg]), np.uint8)
-        rc = self.lib.or_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data, len(keys),
-                                     key_index.ctypes.data if key_index is not None else None, data.ctypes.data,
-                                     offsets.ctypes.data if offsets is not None else None,
-                                     lengths.ctypes.data if lengths is not None else None, count, stride,
-                                     fixed_len, out.ctypes.data)
-        assert rc == 0, rc
-        return out
 
     def chunked(self, alg, msg, chunks):
         """Streaming digest feeding `msg` in pieces of the given size."""
@@ -239,6 +244,9 @@ class Ref(_Batch, _Crc, _Cha):
         self.lib.ref_crc32_batch.argtypes = _CRC_ARGS
         self.fn_crc = self.lib.ref_crc32_batch
         self.lib.ref_crc32_table.argtypes = [_c.c_int, _c.c_void_p]
+        if hasattr(self.lib, "ref_batch_keyed"):
+            self.lib.ref_batch_keyed.argtypes = _KEYED_ARGS
+            self.fn_keyed = self.lib.ref_batch_keyed
 
     def crc32_table(self, variant):
         t = np.zeros(256, np.uint32)

@@ -118,6 +118,73 @@ ref_batch(int alg, const uint8_t *key, size_t key_len, const uint8_t *base,
 	return 0;
 }
 
+/* H(A || B) through the reference's streaming calls: init, update(A),
+ * update(B), final (the keyed-prefix and secret-suffix shapes of RADIUS,
+ * radius.h:774-789 and :1334-1352). */
+static int
+ref_two(int alg, const uint8_t *a, size_t la, const uint8_t *b, size_t lb,
+    uint8_t *out) {
+	switch (alg) {
+	case A_MD5: {
+		md5_ctx_t c;
+		md5_init(&c); md5_update(&c, a, la); md5_update(&c, b, lb);
+		md5_final(&c, out);
+		return 0;
+	}
+	case A_SHA1: {
+		sha1_ctx_t c;
+		sha1_init(&c); sha1_update(&c, a, la); sha1_update(&c, b, lb);
+		sha1_final(&c, out);
+		return 0;
+	}
+	case A_SHA224: case A_SHA256: case A_SHA384: case A_SHA512: {
+		sha2_ctx_t c;
+		sha2_init(ref_bits(alg), &c); sha2_update(&c, a, la);
+		sha2_update(&c, b, lb); sha2_final(&c, out);
+		return 0;
+	}
+	case A_GOST256: case A_GOST512: {
+		gost3411_2012_ctx_t c;
+		gost3411_2012_init(ref_bits(alg), &c);
+		gost3411_2012_update(&c, a, la); gost3411_2012_update(&c, b, lb);
+		gost3411_2012_final(&c, out);
+		return 0;
+	}
+	}
+	return -1;
+}
+
+/* Keyed batch (the shapes of lcb_hash_batch_keyed): message i uses key
+ * key_index[i] (NULL: 0); mode 1 HMAC (the reference's *_hmac_get_digest),
+ * 2 H(K || m), 3 H(m || K).  -2 for a key index out of range. */
+int
+ref_batch_keyed(int alg, int mode, const uint8_t *keys, const uint64_t *key_off,
+    const uint32_t *key_len, size_t nkeys, const uint32_t *key_index,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+    size_t count, uint64_t stride, uint32_t fixed_len, uint8_t *digests) {
+	size_t i, ds = ref_dsize(alg);
+
+	if (0 == ds || mode < 1 || mode > 3)
+		return -1;
+	for (i = 0; i < count; i ++) {
+		const uint8_t *p = base + (offsets ? offsets[i] : (uint64_t)i * stride);
+		size_t n = (lengths ? lengths[i] : fixed_len);
+		uint32_t k = (key_index ? key_index[i] : 0);
+		const uint8_t *K;
+
+		if (k >= nkeys)
+			return -2;
+		K = keys + (key_off ? key_off[k] : 0);
+		if (1 == mode)
+			ref_one_hmac(alg, K, key_len[k], p, n, digests + i * ds);
+		else if (2 == mode)
+			ref_two(alg, K, key_len[k], p, n, digests + i * ds);
+		else
+			ref_two(alg, p, n, K, key_len[k], digests + i * ds);
+	}
+	return 0;
+}
+
 /* Streaming with fixed-size update chunks (chunk 0 = whole message);
  * exercises *_update buffering like gost3411-2012.h:2162-2230. */
 int

@@ -81,3 +81,51 @@ def check_entry(entry, digests):
         assert d.tobytes()[:n].hex() == entry["first"], (entry["name"], entry["alg"])
     if "digest" in entry:
         assert d.tobytes().hex() == entry["digest"], (entry["name"], entry["alg"])
+
+
+# ---------------------------------------------------------------- packets
+# The network-packet shape of the reference's in-tree caller: RADIUS packets
+# of at most 4 KiB (include/proto/radius.h:576) landing at arbitrary receive-
+# buffer offsets (src/threadpool/threadpool_task.c:692-696), one shared
+# secret per peer (src/proto/radius_client.c:242,885,1025).  1M packets,
+# lengths uniform in [20, 4096] (20 = the RADIUS header), packed back to back
+# (byte offsets: every alignment occurs), 64 peer secrets of 8..64 bytes.
+PKT_COUNT = 1 << 20
+PKT_MIN, PKT_MAX = 20, 4096
+PKT_TAG = 0x7061636B65747321      # "packets!": decorrelates the length stream
+PKT_NKEYS = 64
+
+
+def _mix64_np(x):
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def packet_layout(count=PKT_COUNT, seed=SEED):
+    """-> (offsets uint64, lengths uint32, total bytes): packed packets."""
+    with np.errstate(over="ignore"):
+        z = _mix64_np(np.arange(count, dtype=np.uint64) ^ np.uint64(seed ^ PKT_TAG))
+    lens = (np.uint64(PKT_MIN) + z % np.uint64(PKT_MAX - PKT_MIN + 1)).astype(np.uint32)
+    offs = np.zeros(count, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return offs, lens, int(offs[-1]) + int(lens[-1]) if count else 0
+
+
+def packet_keys(nkeys=PKT_NKEYS, seed=SEED):
+    """The peers' shared secrets: key k is the first 8 + (k * 7) % 57 bytes
+    (8..64) of eight mix64 words of its own."""
+    out = []
+    for k in range(nkeys):
+        n = 8 + (k * 7) % 57
+        w = _mix64_np(np.arange(8, dtype=np.uint64) + np.uint64(k * 8) ^ np.uint64(seed ^ 0x6B657973))
+        out.append(w.astype("<u8").view(np.uint8)[:n].tobytes())
+    return out
+
+
+def packet_key_index(count=PKT_COUNT, nkeys=PKT_NKEYS, seed=SEED):
+    """Peer of packet i: mix64 stream mod nkeys (uint32)."""
+    z = _mix64_np(np.arange(count, dtype=np.uint64) ^ np.uint64(seed ^ 0x70656572))
+    return (z % np.uint64(nkeys)).astype(np.uint32)

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Ragged-path A/B driver (GPU box): bench.py's ragged_packets rows (1M packets,
+20..4096 B at byte offsets; plain / HMAC / keyed, reference dod checked), the
+C4 pass, and 1M x 1 KiB described as a ragged batch at strides 1024 / 1040 /
+1025 (aligned, 16-B phase, unaligned).  One JSON line per measurement.
+
+usage: python3 tools/pkt_bench.py [--steps 20] [--algs md5,sha1] [--no-c4]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import liblcb_amd  # noqa: E402
+from liblcb_amd._lib import F_DEVICE, check, lib  # noqa: E402
+
+
+def ragged_1k(stride, steps):
+    count = 1 << 20
+    data = liblcb_amd.gen_synthetic(bench.SEED, count * stride + 64)
+    offs = torch.arange(count, dtype=torch.int64, device="cuda") * stride
+    lens = torch.full((count,), 1024, dtype=torch.int32, device="cuda")
+    dig = torch.empty((count, 16), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def launch():
+        check(lib().lcb_hash_batch(1, None, 0, data.data_ptr(), offs.data_ptr(), lens.data_ptr(), count, 0, 0,
+                                   dig.data_ptr(), F_DEVICE, s.cuda_stream))
+    ms = bench._event_ms(launch, 10, steps, s)
+    return {"variant": "ragged_1k", "stride": stride, "ms": round(ms, 4),
+            "TB_s": round(count * 1024 / (ms * 1e-3) / 1e12, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--algs", default="md5")
+    ap.add_argument("--no-c4", action="store_true")
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    bench.settle()
+    print(json.dumps({"ragged_packets": bench.bench_packets(10, a.steps, tuple(a.algs.split(",")))}), flush=True)
+    for st in (1024, 1040, 1025):
+        print(json.dumps(ragged_1k(st, a.steps)), flush=True)
+    if not a.no_c4:
+        print(json.dumps({"c4": bench.bench_c4(1, 5, a.steps)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
