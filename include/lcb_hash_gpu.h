@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define LCB_HASH_GPU_ABI_VERSION	3
+#define LCB_HASH_GPU_ABI_VERSION	4
 
 /* Algorithm ids. */
 #define LCB_HASH_MD5		1	/* md5.h */
@@ -99,8 +99,9 @@ int	lcb_hash_batch(int alg, const uint8_t *key, size_t key_len,
  * keys, key_offsets and key_lengths are HOST memory.  key_index lives where
  * the batch does (device memory with LCB_HASH_F_DEVICE).  Per-key state
  * (HMAC ipad/opad mid-states, the prefix's whole-block state) is computed
- * once per key on the device.  Host mode: an index >= nkeys is EINVAL;
- * device mode: it selects the last key.  The call waits for the key table
+ * once per key on the device.  An index >= nkeys is EINVAL in both modes and
+ * no digest is written (device mode checks the indices on the device before
+ * the batch runs, read back at the key-table sync).  The call waits for the key table
  * upload (the host arrays may be released on return); with
  * LCB_HASH_F_DEVICE the batch itself stays asynchronous on `stream`.
  */
@@ -178,10 +179,19 @@ int	gost3411_2012_hmac_get_digest_batch(size_t bits, const uint8_t *key,
  * lcb_hash_partition over devs[0..ndev-1] (HIP device ordinals; repeats
  * allowed), all parts concurrently; returns when every digest is written.
  *   flags 0                 host memory, one staging pipeline per part;
+ *                           `stream` ignored;
  *   flags LCB_HASH_F_DEVICE data/offsets/lengths/digests are device memory on
  *                           devs[0]; a part on another device is copied peer-
  *                           to-peer (xGMI), hashed there, and its digests are
- *                           copied back into `digests` on devs[0].
+ *                           copied back into `digests` on devs[0].  `stream`
+ *                           (a hipStream_t of devs[0], NULL = its default
+ *                           stream) orders the call: every part starts after
+ *                           the work enqueued on `stream` before the call (an
+ *                           event recorded there at entry), so the caller may
+ *                           write the batch asynchronously on it and call
+ *                           without a host synchronisation (ABI v4; v3 had no
+ *                           `stream` and required complete inputs).
+ * LCB_HASH_F_COPY_PARTS without LCB_HASH_F_DEVICE is EINVAL.
  * With devs = {d} it equals lcb_hash_batch on device d.  Errors: EINVAL,
  * ENODEV (an ordinal out of range), ENOMEM, EIO. */
 int	lcb_hash_partition(const uint32_t *lengths, size_t count,
@@ -189,7 +199,8 @@ int	lcb_hash_partition(const uint32_t *lengths, size_t count,
 int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
 	    const uint8_t *key, size_t key_len, const uint8_t *data,
 	    const uint64_t *offsets, const uint32_t *lengths, size_t count,
-	    uint64_t stride, uint32_t fixed_len, uint8_t *digests, uint32_t flags);
+	    uint64_t stride, uint32_t fixed_len, uint8_t *digests, uint32_t flags,
+	    void *stream);
 
 /* Synthetic input: writes bytes [start, start+n) of the stream
  * whose u64 word k (little-endian) is mix64(seed ^ k), into device memory. */

@@ -62,7 +62,7 @@ SIGNATURES = [
      [ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp, c_sz, c_vp] + _PLAIN),
     ("lcb_hash_partition", ctypes.c_int, [c_vp, c_sz, c_u32, c_sz, c_vp]),
     ("lcb_hash_batch_multi", ctypes.c_int,
-     [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32]),
+     [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32, c_vp]),
     ("lcb_hash_gen_synthetic", ctypes.c_int, [c_u64, c_u64, c_vp, c_sz, c_vp]),
     ("lcb_hash_gpu_gost_table", ctypes.c_int, [c_vp]),
     ("lcb_hash_gpu_read_probe", ctypes.c_int, [ctypes.c_int, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp]),

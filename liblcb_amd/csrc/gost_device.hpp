@@ -182,6 +182,10 @@ struct GostFlat : GostNaturalOrder {
 // v_perm_b32 (table byte -> address bits 8-15, the lane's bank-pair offset
 // -> bits 0-7), one instruction fewer than the flat form's extract + shift.
 using lds_u8 = __attribute__((address_space(3))) const uint8_t;
+#ifndef LCB_GOST_FENCE
+#define LCB_GOST_FENCE 4
+#endif
+constexpr int kGostLpsFence = LCB_GOST_FENCE;
 using lds_u64 = __attribute__((address_space(3))) const uint64_t;
 
 struct GostRot : GostNaturalOrder {
@@ -190,24 +194,25 @@ struct GostRot : GostNaturalOrder {
     // bank-pair offsets for the 8 steps, packed 4 to a VGPR (v_perm picks the
     // byte), 6 VGPRs fewer than one per step.
     uint32_t offp[2];
-    // Bits 0 / 1 / 2 of r as lane masks (SGPR pairs feeding v_cndmask, not
-    // three all-ones VGPRs).
-    bool b1, b2, b4;
+    // Bits 0 / 1 / 2 of r as all-ones word masks (the barrel's bit-selects are
+    // v_bitop3; as SGPR lane masks feeding v_cndmask the kernel measured ~5 %
+    // slower, tools/ab_gost3.sh).
+    uint32_t m1, m2, m4;
     __device__ __forceinline__ void init(lds_u8* lds) {
         L = lds;
         const uint32_t l = threadIdx.x & 31u, c = l >> 3, r = l & 7u;
         offp[0] = offp[1] = 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) offp[j >> 2] |= ((8u * c + (((uint32_t)j + r) & 7u)) * 8u) << (8 * (j & 3));
-        b1 = (r & 1u) != 0;
-        b2 = (r & 2u) != 0;
-        b4 = (r & 4u) != 0;
+        m1 = (r & 1u) ? 0xffffffffu : 0u;
+        m2 = (r & 2u) ? 0xffffffffu : 0u;
+        m4 = (r & 4u) ? 0xffffffffu : 0u;
     }
     template <int S>
-    __device__ __forceinline__ static void rot(uint32_t (&v)[8], bool m) {  // v[j] <- v[(j + S) & 7] where m
+    __device__ __forceinline__ static void rot(uint32_t (&v)[8], uint32_t m) {  // v[j] <- v[(j + S) & 7] where m
         uint32_t t[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = m ? v[(j + S) & 7] : v[j];
+        for (int j = 0; j < 8; ++j) t[j] = ch3(m, v[(j + S) & 7], v[j]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = t[j];
     }
@@ -216,9 +221,9 @@ struct GostRot : GostNaturalOrder {
         uint32_t lo[8], hi[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { lo[j] = (uint32_t)x[j]; hi[j] = (uint32_t)(x[j] >> 32); }
-        rot<1>(lo, b1); rot<1>(hi, b1);
-        rot<2>(lo, b2); rot<2>(hi, b2);
-        rot<4>(lo, b4); rot<4>(hi, b4);   // lo/hi[j'] = word (j' + r) & 7
+        rot<1>(lo, m1); rot<1>(hi, m1);
+        rot<2>(lo, m2); rot<2>(hi, m2);
+        rot<4>(lo, m4); rot<4>(hi, m4);   // lo/hi[j'] = word (j' + r) & 7
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             uint64_t v[8];
@@ -237,10 +242,10 @@ struct GostRot : GostNaturalOrder {
                               xor3((uint32_t)(v[3] >> 32), (uint32_t)(v[4] >> 32), (uint32_t)(v[5] >> 32)),
                               (uint32_t)(v[6] >> 32) ^ (uint32_t)(v[7] >> 32));
             o[i] = ((uint64_t)h << 32) | l;
-            // Scheduling fence after every 4 output words: bounds the ds_read
-            // lookahead, which otherwise grows until the 128-VGPR budget of the
-            // 4-waves-per-SIMD kernels spills (kernel_resources test).
-            if ((i + 1) % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+            // Scheduling fence after every kGostLpsFence output words: bounds
+            // the ds_read lookahead, which otherwise grows until the 128-VGPR
+            // budget of the 4-waves-per-SIMD kernels spills (kernel_resources test).
+            if (kGostLpsFence && (i + 1) % kGostLpsFence == 0) __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
@@ -255,6 +260,10 @@ __device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
 // than 2^61 bytes; the ABI caps lengths at 2^32): gost3411-2012.h:1110-1144.
 // h and m in the table's lane order (natural order for GostFlat / GostRot;
 // the hooks let tools/gost_half.hpp's lane-ordered layout run the same code).
+#ifndef LCB_GOST_G_ROLLED
+#define LCB_GOST_G_ROLLED 1
+#endif
+#if LCB_GOST_G_ROLLED
 template <class Tab>
 __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
     // E(K, m) as 12 (K, t) steps plus the last key, from K_0 = h, t_0 = m:
@@ -288,42 +297,89 @@ __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_
     for (int i = 0; i < 8; ++i) h[i] ^= t[i] ^ k[i];     // :1142 (h already holds h ^ m)
 }
 
+#else
+// Unrolled head and tail (round 2's form): K_1, t_1 and K_13 outside the
+// 11-round loop.
+template <class Tab>
+__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
+    uint64_t k[8], t[8], x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = h[i];
+    T.xor_n(x, n0);
+    T.lps(k, x);                                         // K = LPS(h ^ N)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x[i] = k[i] ^ m[i];
+        h[i] ^= m[i];
+    }
+    T.lps(t, x);                                         // t = LPS(K ^ m)
+#pragma unroll 1
+    for (int r = 0; r < 11; ++r) {
+        T.xor_c(x, k, r);
+        T.lps(k, x);                                     // K = LPS(K ^ C_r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = t[i] ^ k[i];
+        T.lps(t, x);                                     // t = LPS(t ^ K)
+    }
+    T.xor_c(x, k, 11);
+    T.lps(k, x);                                         // K13 = LPS(K ^ C_11)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= t[i] ^ k[i];     // :1142
+}
+#endif
+
 // The chaining value h is kept in the table's lane order between blocks
 // (natural for the product's tables); Sigma and N in natural order.  The IV (all words equal) reads the
 // same in every order.
 //
-// kSgStride > 0: Sigma lives in LDS (word i of thread x at
-// sgl_base[i * kSgStride + x], bind_sigma), not in VGPRs.  Sigma is touched
-// once per block, and its 16 VGPRs are what pushed the batch kernels (4 waves
-// per SIMD, 128 VGPRs) into scratch spills.
+// kSgLds words of Sigma (the last ones; 0, 4 or 8) live in LDS: word i of
+// thread x at sgl_base[(i - (8 - kSgLds)) * kSgStride + x] (bind_sigma), not
+// in VGPRs.  Sigma is touched once per block, and its 16 VGPRs are what
+// pushed the batch kernels (4 waves per SIMD, 128 VGPRs) into scratch spills.
 using lds_u64w = __attribute__((address_space(3))) uint64_t;
-template <bool k256, int kSgStride = 0>
+template <bool k256, int kSgStride = 0, int kSgLds = 0>
 struct Gost {
     static constexpr int kBlock = 64, kDigest = k256 ? 32 : 64, kWords = 16;
-    uint64_t h[8], n0, sg[kSgStride ? 1 : 8];
-    lds_u64w* sgl;   // kSgStride: this thread's Sigma words (stride kSgStride)
+    static constexpr int kSgReg = 8 - kSgLds;   // Sigma words 0 .. kSgReg-1 in VGPRs
+    // kSgLds == 8: the counter N lives in LDS too (word 8 of the lane's slots).
+    static constexpr bool kNLds = kSgLds == 8;
+    uint64_t h[8], n0, sg[kSgReg ? kSgReg : 1];
+    lds_u64w* sgl;   // kSgLds: this thread's LDS Sigma words (stride kSgStride)
     __device__ __forceinline__ void bind_sigma(lds_u64w* base) {
-        if constexpr (kSgStride) sgl = base + threadIdx.x;
+        if constexpr (kSgLds > 0) sgl = base + threadIdx.x;
     }
     __device__ __forceinline__ uint64_t sigma(int i) const {
-        if constexpr (kSgStride) return sgl[i * kSgStride];
-        else return sg[i];
+        if (i >= kSgReg) return sgl[(i - kSgReg) * kSgStride];
+        return sg[i];
     }
-    // Sigma for the final g_0(h, Sigma), read back from LDS (volatile): else
+    // Sigma for the final g_0(h, Sigma), LDS words read back volatile: else
     // the compiler forwards the words just stored and keeps them in VGPRs
     // through g_0(h, N), which spilled.
     __device__ __forceinline__ uint64_t sigma_final(int i) const {
-        if constexpr (kSgStride) return *(volatile lds_u64w*)&sgl[i * kSgStride];
-        else return sg[i];
+        if (i >= kSgReg) return *(volatile lds_u64w*)&sgl[(i - kSgReg) * kSgStride];
+        return sg[i];
+    }
+    __device__ __forceinline__ uint64_t get_n() const {
+        if constexpr (kNLds) return sgl[8 * kSgStride];
+        else return n0;
+    }
+    __device__ __forceinline__ void set_n(uint64_t v) {
+        if constexpr (kNLds) sgl[8 * kSgStride] = v;
+        else n0 = v;
     }
     __device__ __forceinline__ void set_sigma(int i, uint64_t v) {
-        if constexpr (kSgStride) sgl[i * kSgStride] = v;
+        if (i >= kSgReg) sgl[(i - kSgReg) * kSgStride] = v;
         else sg[i] = v;
     }
     __device__ __forceinline__ void init() {  // gost3411-2012.h:1713-1729
+        // GOST-256's IV word made in place (volatile asm): as a plain constant
+        // the compiler hoists it out of the persistent kernels' message loop
+        // and then spills it.
+        uint32_t iv = 0u;
+        if (k256) asm volatile("v_mov_b32 %0, 0x1010101" : "=v"(iv));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { h[i] = k256 ? 0x0101010101010101ull : 0ull; set_sigma(i, 0); }
-        n0 = 0;
+        for (int i = 0; i < 8; ++i) { h[i] = ((uint64_t)iv << 32) | iv; set_sigma(i, 0); }
+        set_n(0);
     }
     // One g_N step over raw LE words w (gost3411-2012.h:1129-1131).
     // Sigma += m mod 2^512 (gost3411-2012.h:996-1013).
@@ -346,8 +402,8 @@ struct Gost {
         // Sigma first, so that only the lane-ordered copy of m stays live through g_N.
         add_sigma(m);
         T.to_lane(ml, m);
-        gost_g(h, n0, ml, T);
-        n0 += bits;
+        gost_g(h, get_n(), ml, T);
+        set_n(get_n() + bits);
     }
     // Tail + finalisation (gost3411-2012.h:1820-1839).
     template <class Tab>
@@ -355,7 +411,7 @@ struct Gost {
         put_byte(w, rem, 0x01u);
         block(w, (uint64_t)rem * 8u, T);
         uint64_t m[8], ml[8];
-        m[0] = n0;
+        m[0] = get_n();
 #pragma unroll
         for (int i = 1; i < 8; ++i) m[i] = 0;
         T.to_lane(ml, m);
@@ -385,7 +441,8 @@ struct Gost {
             p[2 * i] = (uint32_t)hn[i]; p[2 * i + 1] = (uint32_t)(hn[i] >> 32);
             p[18 + 2 * i] = (uint32_t)sigma(i); p[19 + 2 * i] = (uint32_t)(sigma(i) >> 32);
         }
-        p[16] = (uint32_t)n0; p[17] = (uint32_t)(n0 >> 32);
+        const uint64_t n = get_n();
+        p[16] = (uint32_t)n; p[17] = (uint32_t)(n >> 32);
     }
     template <class Tab>
     __device__ __forceinline__ void load(const uint32_t* p, const Tab& T) {
@@ -396,7 +453,7 @@ struct Gost {
             set_sigma(i, (uint64_t)p[18 + 2 * i] | ((uint64_t)p[19 + 2 * i] << 32));
         }
         T.to_lane(h, hn);
-        n0 = (uint64_t)p[16] | ((uint64_t)p[17] << 32);
+        set_n((uint64_t)p[16] | ((uint64_t)p[17] << 32));
     }
 };
 

@@ -7,28 +7,26 @@
 
 namespace lcbgpu {
 
-__device__ __forceinline__ bool msg_at(const KArgs& a, uint64_t& idx, const uint8_t*& msg, uint64_t& len) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.count) return false;
+__device__ __forceinline__ void msg_at(const KArgs& a, uint64_t i, uint64_t& idx, const uint8_t*& msg,
+                                       uint64_t& len) {
     idx = a.order ? (uint64_t)gptr(a.order)[i] : i;
     msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
     len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
-    return true;
 }
 
 __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
-    return k < a.nkeys ? k : a.nkeys - 1;   // out of range: the last key (documented)
+    return k < a.nkeys ? k : a.nkeys - 1;   // never out of range: lcb_hash_batch_keyed checked the indices
 }
 
-// Message index of this lane, re-derived where the digest is stored (the
-// thread index passes through an empty asm, so the compiler reloads it
-// instead of keeping the 64-bit index live through the whole message: two
-// VGPRs of the 128 the GOST kernels may use).
-__device__ __forceinline__ uint64_t store_index(const KArgs& a) {
+// Message index of message i, re-derived where the digest is stored (i's
+// lane part passes through an empty asm, so the compiler reloads the index
+// instead of keeping it live through the whole message: two VGPRs of the 128
+// the GOST kernels may use).
+__device__ __forceinline__ uint64_t store_index(const KArgs& a, uint64_t base) {
     uint32_t t = threadIdx.x;
     asm volatile("" : "+v"(t));
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
+    const uint64_t i = base + t;
     return a.order ? (uint64_t)gptr(a.order)[i] : i;
 }
 
@@ -41,18 +39,33 @@ __device__ __forceinline__ uint64_t store_index(const KArgs& a) {
 // that spilled 12-68 B per lane to scratch (1.45-1.58x the algorithmic HBM
 // traffic).  (Two 256-thread workgroups at up to 256 VGPRs were 2-3 %
 // slower; tools/gost_lanes_ab.hip)
-constexpr int kGostThreads = 1024;
+#ifndef LCB_GOST_THREADS
+#define LCB_GOST_THREADS 1024
+#endif
+constexpr int kGostThreads = LCB_GOST_THREADS;
+// Sigma words in LDS: all 8 with one 1024-thread workgroup per CU (64 KiB
+// image + 64 KiB Sigma), the last 4 with two 512-thread workgroups (2 x 80 KiB).
+constexpr int kGostSgLds = kGostThreads >= 1024 ? 8 : 4;
+// The grid is persistent: one workgroup per CU stages the image once and
+// walks the batch in strides of (grid x 1024) messages, so no CU idles at a
+// workgroup boundary while its 16 waves drain and the next workgroup stages
+// its table (one resident workgroup per CU: nothing else would fill in).
+#define LCB_GOST_FOR_EACH(a, base)                                                                   \
+    for (uint64_t base = (uint64_t)blockIdx.x * kGostThreads; base < (a).count;                      \
+         base += (uint64_t)gridDim.x * kGostThreads)                                                 \
+        if (base + threadIdx.x < (a).count)
 template <bool k256, bool kHmac>
 __global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
-    __shared__ __attribute__((aligned(16))) uint64_t Sg[8 * kGostThreads];  // Sigma of every lane
+    __shared__ __attribute__((aligned(16))) uint64_t Sg[(kGostSgLds + (kGostSgLds == 8)) * kGostThreads];  // Sigma of every lane
     gost_stage_rot(Timg);
     GostRot T;
     T.init((lds_u8*)Timg);
+    LCB_GOST_FOR_EACH(a, base) {
     uint64_t idx, len;
     const uint8_t* msg;
-    if (!msg_at(a, idx, msg, len)) return;
-    using G = Gost<k256, kGostThreads>;
+    msg_at(a, base + threadIdx.x, idx, msg, len);
+    using G = Gost<k256, kGostThreads, kGostSgLds>;
     G st;
     st.bind_sigma((lds_u64w*)Sg);
     uint32_t dw[G::kDigest / 4];
@@ -66,21 +79,23 @@ __global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
         gost_run(st, GostPlainSrc{msg, len}, T);
     }
     st.digest_words(dw, T);
-    store_digest<G::kDigest>(a.digests + store_index(a) * G::kDigest, dw);
+    store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
+    }
 }
 
 // Keyed GOST batches (see md_keyed_kernel).
 template <bool k256, int kMode>
 __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];
-    __shared__ __attribute__((aligned(16))) uint64_t Sg[8 * kGostThreads];
+    __shared__ __attribute__((aligned(16))) uint64_t Sg[(kGostSgLds + (kGostSgLds == 8)) * kGostThreads];
     gost_stage_rot(Timg);
     GostRot T;
     T.init((lds_u8*)Timg);
+    LCB_GOST_FOR_EACH(a, base) {
     uint64_t idx, len;
     const uint8_t* msg;
-    if (!msg_at(a, idx, msg, len)) return;
-    using G = Gost<k256, kGostThreads>;
+    msg_at(a, base + threadIdx.x, idx, msg, len);
+    using G = Gost<k256, kGostThreads, kGostSgLds>;
     const uint32_t k = key_of(a, idx);
     const uint32_t* mid = gptr(a.mid) + (uint64_t)k * 2 * kMidWords;
     const uint8_t* K = gptr(a.keys) + gptr(a.key_off)[k];
@@ -93,7 +108,7 @@ __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
         gost_run(st, GostPlainSrc{msg, len}, T);
         st.digest_words(dw, T);
         // The key's outer mid-state, looked up again (not kept live through the message).
-        const uint64_t i2 = store_index(a);
+        const uint64_t i2 = store_index(a, base);
         gost_outer(st, dw, gptr(a.mid) + (uint64_t)key_of(a, i2) * 2 * kMidWords + kMidWords, T);
     } else if (kMode == kKeyPrefix) {
         // State after K's whole blocks; the rest of K and the message as one
@@ -106,7 +121,8 @@ __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
         gost_run(st, GostVirtSrc{msg, len, K, kl}, T);
     }
     st.digest_words(dw, T);
-    store_digest<G::kDigest>(a.digests + store_index(a) * G::kDigest, dw);
+    store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
+    }
 }
 
 // One lane per key (flat table; the whole block stages it first).
@@ -189,15 +205,20 @@ __global__ __launch_bounds__(256) void gost_hmac_prep_kernel(KeyBlock kb, const 
     st.save(mid + kMidWords, T);
 }
 
+static dim3 gost_grid(uint64_t count) {
+    const uint64_t need = (count + kGostThreads - 1) / kGostThreads;
+    const uint64_t cus = (uint64_t)device_cu_count();
+    return dim3((unsigned)(need < cus ? need : cus));
+}
 template <bool k256>
 void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
-    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
+    const dim3 g = gost_grid(a.count);
     if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), g, dim3(kGostThreads), 0, s, a);
     else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), g, dim3(kGostThreads), 0, s, a);
 }
 template <bool k256>
 void launch_gost_keyed(const KArgs& a, hipStream_t s) {
-    const dim3 g((unsigned)((a.count + kGostThreads - 1) / kGostThreads));
+    const dim3 g = gost_grid(a.count);
     switch (a.key_mode) {
     case kKeyHmac: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyHmac>), g, dim3(kGostThreads), 0, s, a); break;
     case kKeyPrefix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyPrefix>), g, dim3(kGostThreads), 0, s, a); break;

@@ -232,13 +232,27 @@ struct Md5 {
     static constexpr bool kPairLoad = true;   // HBM-bound: read whole 128-B lines
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = false;  // no schedule to move: pad block via compress()
-    static constexpr int kTileOcc = 7;         // md_tiles_kernel: waves per SIMD (0: not used)
+    static constexpr int kTileOcc = 4;         // md_tiles_kernel: waves per SIMD (0: not used)
     uint32_t s[4];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
     }
+    // x + T as one v_add_u32 with T as an inline literal, the asm hiding the
+    // constant from loop-invariant code motion: in a kernel with several
+    // inlined compressions in loops (md_tiles_kernel) the compiler otherwise
+    // parks all 64 T in SGPRs, which pushed its other scalars into VGPR lanes
+    // and its VGPRs into scratch.
+    template <uint32_t T>
+    __device__ __forceinline__ static uint32_t addk(uint32_t x) {
+        uint32_t r;
+        asm("v_add_u32 %0, %1, %2" : "=v"(r) : "i"(T), "v"(x));
+        return r;
+    }
 #define LCB_MD5_STEP(f, a, b, c, d, x, t, r) \
-    a = b + rotl32(a + (f) + (x) + (t), r)
+    a = b + rotl32(kLit ? addk<t>(a + (f) + (x)) : a + (f) + (x) + (t), r)
+    // kLit: T added last through addk (see there; after a + F + x, so the asm
+    // cannot be hoisted ahead of its step either).
+    template <bool kLit = true>
     __device__ __forceinline__ void compress(const uint32_t* w) {
         uint32_t a = s[0], b = s[1], c = s[2], d = s[3];
 #define F1(b, c, d) ch3((b), (c), (d))

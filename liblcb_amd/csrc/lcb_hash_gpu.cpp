@@ -121,14 +121,14 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     // The bucketing permutation holds message indices as uint32.
     if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
-        // work: [key histogram | key fill counters | tile-queue head | count order]
-        const size_t bytes = (kBucketWork + a.count) * sizeof(uint32_t);
+        // work: [key histogram | key fill counters | tile-queue head | tile count | order]
+        const size_t bytes = bucket_words(a.count) * sizeof(uint32_t);
         if (work_buf) {
             work = work_buf;
         } else {
             LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&work), bytes, s));
         }
-        launch_bucketing(a, work, work + kBucketWork, s);
+        launch_bucketing(a, work, work + kBucketWork, tiles_take(alg, a), s);
         a.tile_next = work + kBucketHead;
         a.order = work + kBucketWork;
     }
@@ -545,7 +545,10 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = nkeys * 4;
     const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
     uint8_t* dbuf = nullptr;
-    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b, s));
+    // [key bytes | key offsets | key lengths | mid-states | bad-index word]
+    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b + 16, s));
+    uint32_t* d_bad = reinterpret_cast<uint32_t*>(dbuf + blob_b + 2 * tab_b + mid_b);
+    uint32_t h_bad = 0;
     KeyTable kt;
     kt.mode = (uint32_t)key_mode;
     kt.keys = dbuf;
@@ -566,7 +569,20 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
         launch_key_prep(alg, a, const_cast<uint32_t*>(kt.mid), s);
         rc = map_err(hipGetLastError());
     }
+    // Device mode: an out-of-range key index is found on the device before
+    // the batch runs and read back at the sync the key upload needs anyway:
+    // EINVAL and no digest written, as in host mode.
+    if (!rc && dev_mode && key_index) {
+        if (hipMemsetAsync(d_bad, 0, 4, s) != hipSuccess) rc = EIO;
+        if (!rc) {
+            launch_key_check(key_index, count, (uint32_t)nkeys, d_bad, s);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(&h_bad, d_bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+                rc = EIO;
+        }
+    }
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EIO;
+    if (!rc && h_bad) rc = EINVAL;
     if (!rc) {
         rc = dev_mode ? batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s,
                                      nullptr, &kt)

@@ -103,10 +103,13 @@ struct DevPart {
     uint8_t* dig = nullptr;
 };
 
+// `ready`: an event on the home device recorded on the caller's stream at
+// entry; every part's stream waits on it before touching the batch, so the
+// parts run after the caller's earlier work on its stream (ABI v4).
 int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, size_t key_len,
                  const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, uint64_t stride,
                  uint32_t fixed_len, uint8_t* digests, const std::vector<uint64_t>& h_off,
-                 const std::vector<uint32_t>& h_len, bool copy_all) {
+                 const std::vector<uint32_t>& h_len, bool copy_all, hipEvent_t ready) {
     const size_t D = dsize(alg);
     const int home = parts[0].dev;
     std::vector<DevPart> dp(parts.size());
@@ -119,7 +122,9 @@ int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, si
         if (p.hi <= p.lo) continue;
         const uint64_t n = p.hi - p.lo;
         DevPart& q = dp[k];
-        if (fail(hipSetDevice(p.dev)) || fail(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking))) break;
+        if (fail(hipSetDevice(p.dev)) || fail(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking)) ||
+            fail(hipStreamWaitEvent(q.s, ready, 0)))
+            break;
         if (p.dev == home && !(copy_all && k > 0)) {  // in place on the home device
             rc = batch_device(alg, key, key_len, offsets ? data : data + p.lo * stride,
                               offsets ? offsets + p.lo : nullptr, lengths ? lengths + p.lo : nullptr, n,
@@ -192,10 +197,11 @@ int lcb_hash_partition(const uint32_t* lengths, size_t count, uint32_t fixed_len
 
 int lcb_hash_batch_multi(const int* devs, int ndev, int alg, const uint8_t* key, size_t key_len,
                          const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, size_t count,
-                         uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags) {
+                         uint64_t stride, uint32_t fixed_len, uint8_t* digests, uint32_t flags, void* stream) {
     if (!devs || ndev <= 0 || ndev > 64) return EINVAL;
     if (alg < LCB_HASH_MD5 || alg > LCB_HASH_GOST512) return EINVAL;
     if (flags & ~(LCB_HASH_F_DEVICE | LCB_HASH_F_COPY_PARTS)) return EINVAL;
+    if ((flags & LCB_HASH_F_COPY_PARTS) && !(flags & LCB_HASH_F_DEVICE)) return EINVAL;
     if (count == 0) return 0;
     if (!data || !digests) return EINVAL;
     if (key == nullptr && key_len != 0) return EINVAL;
@@ -205,35 +211,47 @@ int lcb_hash_batch_multi(const int* devs, int ndev, int alg, const uint8_t* key,
     for (int k = 0; k < ndev; ++k)
         if (devs[k] < 0 || devs[k] >= ndevices) return ENODEV;
     const bool dev_mode = flags & LCB_HASH_F_DEVICE;
-    // Device mode: the partition (and the remote parts' rebasing) needs the
-    // offsets / lengths on the host.
     std::vector<uint64_t> h_off;
     std::vector<uint32_t> h_len;
     const uint32_t* plen = lengths;
-    if (dev_mode && (offsets || lengths)) {
+    hipEvent_t ready = nullptr;
+    if (dev_mode) {
+        // The batch is on devs[0], written by the caller's earlier work on
+        // `stream`: the offsets / lengths the partition (and the remote parts'
+        // rebasing) needs are copied out on that stream, and an event recorded
+        // there gates every part (include/lcb_hash_gpu.h, ABI v4).
         int cur = 0;
         (void)hipGetDevice(&cur);
         if (hipSetDevice(devs[0]) != hipSuccess) return ENODEV;
-        hipError_t e = hipSuccess;
-        if (offsets) {
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        hipError_t e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+        if (e == hipSuccess && offsets) {
             h_off.resize(count);
-            e = hipMemcpy(h_off.data(), offsets, count * 8, hipMemcpyDeviceToHost);
+            e = hipMemcpyAsync(h_off.data(), offsets, count * 8, hipMemcpyDeviceToHost, s);
         }
         if (e == hipSuccess && lengths) {
             h_len.resize(count);
-            e = hipMemcpy(h_len.data(), lengths, count * 4, hipMemcpyDeviceToHost);
+            e = hipMemcpyAsync(h_len.data(), lengths, count * 4, hipMemcpyDeviceToHost, s);
         }
+        if (e == hipSuccess) e = hipEventRecord(ready, s);
+        if (e == hipSuccess && (offsets || lengths)) e = hipEventSynchronize(ready);
         (void)hipSetDevice(cur);
-        if (e != hipSuccess) return map_err(e);
+        if (e != hipSuccess) {
+            if (ready) (void)hipEventDestroy(ready);
+            return map_err(e);
+        }
         plen = lengths ? h_len.data() : nullptr;
     }
     std::vector<uint64_t> first(ndev + 1);
     partition(plen, count, fixed_len, (size_t)ndev, first.data());
     std::vector<Part> parts(ndev);
     for (int k = 0; k < ndev; ++k) parts[k] = Part{devs[k], first[k], first[k + 1]};
-    if (dev_mode)
-        return multi_device(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests,
-                            h_off, h_len, flags & LCB_HASH_F_COPY_PARTS);
+    if (dev_mode) {
+        const int rc = multi_device(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests,
+                                    h_off, h_len, flags & LCB_HASH_F_COPY_PARTS, ready);
+        (void)hipEventDestroy(ready);   // every part has been synchronised
+        return rc;
+    }
     return multi_host(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests);
 }
 

@@ -423,7 +423,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_off), msgs * 8));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_len), msgs * 4));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_dig), msgs * D));
-    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), (kBucketWork + msgs) * sizeof(uint32_t)));
+    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), bucket_words(msgs) * sizeof(uint32_t)));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
     b.leases = new (std::nothrow) LeaseRec[nleases];
@@ -439,7 +439,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
         hipMemcpyAsync(b.d_off, b.h_off, msgs * 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemcpyAsync(b.d_len, b.h_len, msgs * 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemsetAsync(b.d_dig, 0, msgs * D, b.stream) != hipSuccess ||
-        hipMemsetAsync(b.d_work, 0, (kBucketWork + msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
+        hipMemsetAsync(b.d_work, 0, bucket_words(msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
         hipMemcpyAsync(b.h_dig, b.d_dig, msgs * D, hipMemcpyDeviceToHost, b.stream) != hipSuccess ||
         hipStreamSynchronize(b.stream) != hipSuccess)
         return EIO;

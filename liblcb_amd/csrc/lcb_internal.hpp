@@ -56,14 +56,27 @@ struct KeyBlock {
 };
 
 // Bucket keys of ragged-batch bucketing (see lcb_kernels.hip): a length
-// class (< 128) and the record's 64-B half-line phase, key = class * 2 + half.
-constexpr int kBucketKeys = 256;
+// class (< 122) times 6 start phases: 0 / 1 = a 16-B aligned record starting
+// in the first / second half of a 128-B line, 2 + q = a record at 4-B phase q
+// of a 16-B chunk with any byte offset beyond it (q = (start >> 2) & 3).
+constexpr int kBucketClasses = 122;
+constexpr int kBucketPhases = 6;
+constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
 // Bucketing scratch ahead of the permutation: key histogram, per-key fill
-// counters, the tile-queue head (uint32 words).
+// counters, the tile-queue head, the number of 64-entry tiles (uint32 words).
 constexpr int kBucketHead = 2 * kBucketKeys;
-constexpr int kBucketWork = 2 * kBucketKeys + 1;
+constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
+constexpr int kBucketWork = 2 * kBucketKeys + 2;
 // Ragged batches at least this large are bucketed by length first.
 constexpr uint64_t kBucketMinCount = 4096;
+// When every key has enough messages (count >= kBucketPadRatio * 64 * keys
+// in use), each key's run of `order` is padded to a whole number of tiles
+// with kOrderPad entries, so no tile mixes keys (at most 63 per key).
+constexpr uint32_t kOrderPad = 0xffffffffu;
+constexpr uint64_t kBucketPadRatio = 16;
+// uint32 words of bucketing scratch for a batch of `count` messages
+// ([work | order], order padded).
+inline size_t bucket_words(uint64_t count) { return (size_t)kBucketWork + count + 63ull * kBucketKeys; }
 
 // CRC-32 variants travel through the batch machinery as alg ids
 // kCrcAlgBase + variant (variant ids of include/lcb_crc32_gpu.h).
@@ -117,14 +130,20 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
 void launch_crc(int variant, const KArgs& a, hipStream_t s);
 void crc_table_host(int variant, uint32_t* out);
 // Bucketing permutation of the ragged batch `a` (reads data/offsets/stride/
-// lengths/count) into `order`; `work` = kBucketWork words (histogram, fill
-// counters, tile-queue head), zeroed here.
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream_t s);
+// lengths/count) into `order` (bucket_words(count) - kBucketWork words,
+// padded per key when the batch is large); `work` = kBucketWork words
+// (histogram, fill counters, tile-queue head, tile count), zeroed here.
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allow_pad, hipStream_t s);
+// True when launch_batch(alg, a) runs the tile kernel on a bucketed batch:
+// only then may `order` hold pad entries (every other kernel reads it per lane).
+bool tiles_take(int alg, const KArgs& a);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
                       uint32_t* mid, hipStream_t s);
 // Key-table prep of a keyed batch: mid[k] for every key (kKeyHmac, kKeyPrefix).
 void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s);
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
+// *bad |= 1 if any of idx[0..count) >= nkeys (bad zeroed by the caller).
+void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, hipStream_t s);
 // HBM read probes (lcb_hash_gpu_read_probe): mode 0 = the fixed-stride line
 // stream alone over `a`'s records, mode 1 = linear coalesced read of
 // count * stride bytes; sink: one uint32 per record (0) / per thread (1).
@@ -149,7 +168,7 @@ hipError_t scratch_free(void* p, hipStream_t s);
 int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
                uint8_t** dkey_out);
 // Batch kernel launch, bucketing a large ragged batch by length first.
-// work_buf: optional caller-owned device buffer of (kBucketWork + count)
+// work_buf: optional caller-owned device buffer of bucket_words(count)
 // uint32 for the bucketing of a ragged batch; null = stream-ordered allocation.
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf = nullptr);
 

@@ -104,15 +104,19 @@ void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s) {
 // Ragged batches: lanes of one wavefront run until the longest lane's message
 // is done, so a random mix of 64 B and 64 KiB messages would make almost
 // every wave as slow as a 64 KiB one.  These kernels compute a permutation
-// `order` that groups messages by block-count class, longest class first
-// (a counting sort; order inside a class is arbitrary and does not affect
-// any digest, which is always written at the message's own index).
+// `order` that groups messages by key = length class x start phase, highest
+// key (longest class) first (a counting sort; order inside a key is arbitrary
+// and does not affect any digest, which is always written at the message's
+// own index):
 //   class(len) = nb for nb = len/64 + 1 < 64, else 58 + floor(log2(nb))
-// i.e. exact block counts up to 4 KiB, power-of-two bins above.  Inside a
-// class, records whose start lies in the first half of a 128-B line come
-// after those in the second half (key = class * 2 + half): tiles of 64
-// consecutive entries then share their half-line phase, and the tile kernel
-// streams a 64-B-phase tile as whole cache lines (md_tile_stream).
+//   (exact block counts up to 4 KiB, power-of-two bins above), and
+//   phase     = 0 / 1 for a 16-B aligned start in the first / second half of
+//               a 128-B line (the tile kernel streams those tiles as whole
+//               cache lines), else 2 + ((start >> 2) & 3): the 4-B phase q
+//               inside the record's first 16-B chunk, which the tile
+//               kernel's byte-shifting line stream needs uniform per wave.
+// Tiles of 64 consecutive `order` entries then share their key.  For a large
+// batch every key's run is padded to whole tiles with kOrderPad entries.
 __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     const uint64_t nb = (len >> 6) + 1;
     if (nb < 64) return (uint32_t)nb;
@@ -121,8 +125,9 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
 
 __device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
     const uint64_t off = a.offsets ? gptr(a.offsets)[i] : i * a.stride;
-    const uint32_t half = (uint32_t)(((reinterpret_cast<uintptr_t>(a.data) + off) >> 6) & 1u);
-    return (len_class(gptr(a.lengths)[i]) << 1) | half;
+    const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(a.data) + off);
+    const uint32_t ph = (p & 15u) == 0 ? ((p >> 6) & 1u) : 2u + ((p >> 2) & 3u);
+    return len_class(gptr(a.lengths)[i]) * kBucketPhases + ph;
 }
 
 // Few, large blocks (kBucketBlocks x 1024 threads): every block adds its LDS
@@ -143,49 +148,70 @@ __global__ __launch_bounds__(1024) void bucket_hist_kernel(KArgs a, uint32_t* hi
         if (h[c]) atomicAdd(&hist[c], h[c]);
 }
 
-// Block b owns the contiguous chunk [b * chunk, (b + 1) * chunk): it counts
-// its keys, reserves one range per key (start of the key in DESCENDING key
-// order, from the global histogram, + a per-key fill counter), then places
-// its indices (LDS atomics give the rank inside the block's range).
+static_assert(kBucketKeys <= 1024, "one scan element per thread");
+
+// Block b owns the contiguous chunk [b * chunk, (b + 1) * chunk).  Every block
+// derives the start of each key's run (DESCENDING key order, runs padded to
+// whole tiles when the batch is large) from the global histogram with one
+// 1024-wide LDS scan, counts its own keys, reserves one range per key (fill
+// counter atomics), then places its indices (LDS atomics give the rank inside
+// the block's range).  Block 0 also writes the pad entries and the tile count.
 __global__ __launch_bounds__(1024) void bucket_scatter_kernel(KArgs a, const uint32_t* hist, uint32_t* fill,
-                                                             uint32_t* order, uint64_t chunk) {
+                                                             uint32_t* ntiles, uint32_t* order, uint64_t chunk,
+                                                             bool allow_pad) {
     __shared__ uint32_t h[kBucketKeys];
-    __shared__ uint32_t base[kBucketKeys];
-    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
+    __shared__ uint32_t base[1024];
+    const uint32_t t = threadIdx.x;
+    // Scan element t = key kBucketKeys - 1 - t (descending), padded count.
+    const int kt = (int)kBucketKeys - 1 - (int)t;
+    const uint32_t hk = kt >= 0 ? hist[kt] : 0u;
+    const int used = __syncthreads_count(hk != 0);
+    const bool pad = allow_pad && a.count >= kBucketPadRatio * 64 * (uint64_t)used;
+    const uint32_t len = pad ? (hk + 63u) & ~63u : hk;
+    base[t] = len;
+    for (int c = t; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {     // inclusive scan (Hillis-Steele)
+        const uint32_t v = t >= d ? base[t - d] : 0u;
+        __syncthreads();
+        base[t] += v;
+        __syncthreads();
+    }
+    const uint32_t start = base[t] - len;          // exclusive
+    __syncthreads();
+    if (kt >= 0) {
+        if (blockIdx.x == 0) {
+            for (uint32_t e = start + hk; e < start + len; ++e) order[e] = kOrderPad;
+            if (t == 0) *ntiles = base[1023];   // entries of `order`, pads included
+        }
+        base[t] = start;                           // base of key kt at scan slot t
+    }
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&h[bucket_key(a, i)], 1u);
+    for (uint64_t i = lo + t; i < hi; i += blockDim.x) atomicAdd(&h[bucket_key(a, i)], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int c = kBucketKeys - 1; c >= 0; --c) {
-            base[c] = run;
-            run += hist[c];
-        }
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < kBucketKeys; k += blockDim.x) {
-        if (h[k]) base[k] += atomicAdd(&fill[k], h[k]);
+    for (int k = t; k < kBucketKeys; k += blockDim.x) {
+        const uint32_t slot = (uint32_t)(kBucketKeys - 1 - k);
+        if (h[k]) base[slot] += atomicAdd(&fill[k], h[k]);
         h[k] = 0;
     }
     __syncthreads();
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    for (uint64_t i = lo + t; i < hi; i += blockDim.x) {
         const uint32_t k = bucket_key(a, i);
-        order[base[k] + atomicAdd(&h[k], 1u)] = (uint32_t)i;
+        order[base[kBucketKeys - 1 - k] + atomicAdd(&h[k], 1u)] = (uint32_t)i;
     }
 }
 
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream_t s) {
-    // work: histogram | fill counters | tile-queue head, zeroed here; order:
-    // count uint32.
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allow_pad, hipStream_t s) {
+    // work: histogram | fill counters | tile-queue head | tile count, zeroed
+    // here; order: bucket_words(count) - kBucketWork uint32.
     (void)hipMemsetAsync(work, 0, kBucketWork * sizeof(uint32_t), s);
     uint64_t nb = (a.count + 1023) / 1024;
     if (nb > kBucketBlocks) nb = kBucketBlocks;
     const uint64_t chunk = (a.count + nb - 1) / nb;
     hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a, work);
     hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((a.count + chunk - 1) / chunk)), dim3(1024), 0, s, a,
-                       work, work + kBucketKeys, order, chunk);
+                       work, work + kBucketKeys, work + kBucketNTiles, order, chunk, allow_pad);
 }
 
 // ------------------------------------------------------------- dispatch
@@ -201,6 +227,30 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, hipStream
     case 8: fn##_gost512(__VA_ARGS__); break;                     \
     default: break;                                               \
     }
+
+// Keyed batches, device mode: flags an out-of-range key index before the
+// batch runs (lcb_hash_batch_keyed returns EINVAL then and writes no digest,
+// as host mode does).  One global atomic OR per offending lane.
+__global__ __launch_bounds__(256) void key_index_check_kernel(const uint32_t* idx, uint64_t count, uint32_t nkeys,
+                                                              uint32_t* bad) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        if (gptr(idx)[i] >= nkeys) __hip_atomic_fetch_or(gptr(bad), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, hipStream_t s) {
+    uint64_t blocks = (count + 255) / 256;
+    const uint64_t cap = (uint64_t)4 * device_cu_count();
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(key_index_check_kernel, dim3((unsigned)(blocks ? blocks : 1)), dim3(256), 0, s, idx, count,
+                       nkeys, bad);
+}
+
+bool tiles_take(int alg, const KArgs& a) {
+    // MD5 (the only hash with a tile kernel, Md5::kTileOcc): plain, HMAC,
+    // keyed HMAC and keyed suffix batches (md_kernels.hpp launch_md*).
+    return alg == 1 && a.key_mode != kKeyPrefix;
+}
 
 void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s) {
     LCB_ALG_SWITCH(launch_key_prep, a, mid, s)

@@ -136,166 +136,9 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
 }
 
-// ------------------------------------- MD family, bucketed ragged batches
-// A length-bucketed batch (`order` lists messages longest class first) is cut
-// into TILES of 64 consecutive `order` entries, one tile per wave at a time,
-// in a persistent grid of 5-wave workgroups sized to what is resident
-// (5 per CU: 25 waves):
-//   waves 0..3  STREAM waves: when every record of the tile has the same
-//               number of whole 128-B lines (a length bucket) and starts 16-B
-//               aligned, the lines move through an 8 KiB LDS slab per wave
-//               by coalesced LDS-DMA (GatherLineStream: 8 records x one line
-//               per instruction); other tiles load per lane;
-//   wave 4      a DIRECT wave: per-lane 128-B line loads, no LDS.
-// LDS holds 4 x 5 = 20 stream waves per CU (5,120 on the chip); a C4 batch
-// (1M records of {64 B, 1 KiB, 64 KiB}) has 5,461 tiles of
-// 64 KiB records, so with stream waves alone the last 341 long tiles start
-// only when the first ones end (profiles/r1_gather_ab.txt).  Here every
-// wave's FIRST tile is static — stream waves take tiles 0 .. S-1, direct
-// waves S .. S+D-1 (S, D = resident stream / direct waves) — so all 5,461
-// long chains start at once, and later tiles come from one device-scope
-// atomic queue head, longest first.  Every wave leaves the loop once the
-// queue is past the last tile.  Measured on C4 (MD5, profiles/r2_c4_tiles_ab.txt):
-// 4.81 ms against 5.20-5.25 for the per-lane kernel and 4.92 for stream
-// waves alone; 6-wave workgroups (5 + 1, 80 VGPRs) 5.54.
-template <class H, bool kHmac>
-__device__ __forceinline__ void md_tile_finish(const KArgs& a, H& st, uint64_t idx, const uint8_t* msg, uint64_t len,
-                                               uint64_t done, uint64_t prefix) {
-    md_message(st, msg + done, len - done, prefix + done);
-    uint32_t dw[H::kDigest / 4];
-    st.digest_words(dw);
-    if (kHmac) {
-        H o;
-        load_words(o.s, a.mid + kMidWords);
-        md_outer(o, dw);
-        o.digest_words(dw);
-    }
-    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
-}
-
-// One 128-B line: two 64-B blocks, or one SHA-384/512 block.
-template <class H>
-__device__ __forceinline__ void md_compress_line(H& st, const uint32_t* w) {
-    if constexpr (H::kBlock == 128) {
-        st.compress(w);
-    } else {
-        st.compress(w);
-        st.compress(w + 16);
-    }
-}
-
-// Record `i` (clamped to the batch) of a bucketed batch: index, start, length.
-__device__ __forceinline__ void tile_record(const KArgs& a, uint64_t i, uint64_t& idx, const uint8_t*& msg,
-                                            uint64_t& len) {
-    const uint64_t last = a.count - 1;
-    idx = gptr(a.order)[i > last ? last : i];
-    msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
-    len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
-}
-
-template <class H, bool kHmac>
-__device__ __forceinline__ void md_tile_stream(const KArgs& a, uint64_t first, uint32_t lane, uint8_t* slab) {
-    const uint64_t last = a.count - 1, i = first + lane;
-    uint64_t idx, len;
-    const uint8_t* msg;
-    tile_record(a, i, idx, msg, len);
-    H st;
-    uint64_t prefix = 0;
-    if (kHmac) {
-        load_words(st.s, a.mid);
-        prefix = H::kBlock;
-    } else {
-        st.init();
-    }
-    // Lines streamed per record; lanes past the end repeat the last record
-    // (clamped above) and discard it.
-    const uint32_t nl = (uint32_t)((len >> 7) < 0xffffffu ? (len >> 7) : 0xffffffu);
-    // Stream when every record of the tile has the same number (> 0) of
-    // whole lines and starts 16-B aligned (a length bucket: C4's 64 KiB
-    // tiles); otherwise every lane loads its own bytes.
-    const bool ok = nl > 0 && (reinterpret_cast<uintptr_t>(msg) & 15u) == 0 &&
-                    nl == (uint32_t)__builtin_amdgcn_readfirstlane(nl);
-    uint64_t done = 0;
-    if (__all(ok)) {  // wave-uniform
-        const uint32_t nlu = (uint32_t)__builtin_amdgcn_readfirstlane(nl);
-        // Half-line phase of the tile (bucketing groups it): 0 when every
-        // record starts on a 128-B line, 1 when every record starts 64 B into
-        // one, 2 otherwise.
-        const uint32_t ma = (uint32_t)reinterpret_cast<uintptr_t>(msg) & 127u;
-        const uint32_t ma0 = (uint32_t)__builtin_amdgcn_readfirstlane(ma);
-        const uint32_t ph = (__all(ma == ma0) && (ma0 & 63u) == 0) ? (ma0 >> 6) : 2u;
-        GatherLineStream gs;
-        if (H::kBlock == 64 && ph < 2) {
-            // Whole cache lines: a 64-B-phase tile streams the nlu + 1 lines
-            // its records overlap (line L = blocks 2L-1 and 2L of the record;
-            // the bytes before its first block and after its last whole line
-            // share those cache lines and are discarded), so no line is read
-            // twice and the stream carries the read-once (nt) policy.
-            const uint32_t n = nlu + ph;
-            gs.init_gather(msg - 64 * ph, n - 1, lane, slab);
-            gs.issue_next_uniform<kLdsAux>();
-            for (uint32_t L = 0; L < n; ++L) {
-                uint32_t w[32];
-                gs.take(w, w + 16);
-                if (L + 1 < n) gs.issue_next_uniform<kLdsAux>();
-                if (ph == 0 || L > 0) st.compress(w);
-                if (ph == 0 || L < nlu) st.compress(w + 16);
-            }
-        } else {
-            gs.init_gather(msg, nlu - 1, lane, slab);
-            gs.issue_next_uniform();
-            for (uint32_t L = 0; L < nlu; ++L) {
-                uint32_t w[32];
-                gs.take(w, w + 16);
-                if (L + 1 < nlu) gs.issue_next_uniform();
-                md_compress_line(st, w);
-            }
-        }
-        done = (uint64_t)nlu * 128;
-    }
-    if (i > last) return;
-    tile_record(a, i, idx, msg, len);   // reloaded: not kept live across the line loop
-    md_tile_finish<H, kHmac>(a, st, idx, msg, len, done, prefix);
-}
-
-template <class H, bool kHmac>
-__device__ __forceinline__ void md_tile_direct(const KArgs& a, uint64_t first, uint32_t lane) {
-    const uint64_t i = first + lane;
-    if (i >= a.count) return;
-    const uint64_t idx = gptr(a.order)[i];
-    const uint8_t* msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
-    const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[idx] : (uint64_t)a.fixed_len;
-    H st;
-    uint64_t prefix = 0;
-    if (kHmac) {
-        load_words(st.s, a.mid);
-        prefix = H::kBlock;
-    } else {
-        st.init();
-    }
-    md_tile_finish<H, kHmac>(a, st, idx, msg, len, 0, prefix);
-}
-
-constexpr int kTileWaves = 5;         // waves per workgroup: 4 stream waves (32 KiB LDS) + 1 direct wave
-constexpr int kTileStreamWaves = 4;
-constexpr int kTileWgPerCu = 5;       // 160 KiB of LDS / 32 KiB; 25 waves per CU (7 on one SIMD)
-
-template <class H, bool kHmac>
-__global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nstream, uint32_t nwaves) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kTileStreamWaves][8192];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const bool stream = wv < (uint32_t)kTileStreamWaves;   // wave-uniform
-    const uint64_t ntiles = (a.count + 63) / 64;
-    uint64_t t = stream ? (uint64_t)blockIdx.x * kTileStreamWaves + wv
-                        : (uint64_t)nstream + (uint64_t)blockIdx.x * (kTileWaves - kTileStreamWaves) + (wv - kTileStreamWaves);
-    while (t < ntiles) {
-        if (stream) md_tile_stream<H, kHmac>(a, t * 64, lane, &slab[wv][0]);
-        else md_tile_direct<H, kHmac>(a, t * 64, lane);
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(a.tile_next, 1u);   // device scope, returns the old head
-        t = (uint64_t)nwaves + __builtin_amdgcn_readfirstlane(c);
-    }
-}
+}  // namespace lcbgpu
+#include "md_tiles.hpp"
+namespace lcbgpu {
 
 // HMAC key schedule on the device (RFC 2104, md5.h:309-338): key block =
 // key (<= B bytes, passed by value) or H(key) (long key in device memory);
@@ -338,10 +181,6 @@ __global__ __launch_bounds__(64) void md_hmac_prep_kernel(KeyBlock kb, const uin
 //           the rest of K_k and m_i are hashed as one virtual message
 //           (radius.h:774-789: the key-prefixed MD5 context copied per block);
 // kKeySuffix H(m_i || K_k) (radius.h:1334-1336, 1346-1352).
-__device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
-    const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
-    return k < a.nkeys ? k : a.nkeys - 1;   // out of range: the last key (documented)
-}
 
 template <class H, int kMode>
 __global__ __launch_bounds__(256, H::kBlock == 128 ? 3 : (H::kOcc < 4 ? H::kOcc : 4)) void md_keyed_kernel(KArgs a) {
@@ -434,21 +273,8 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
             return;
         }
     }
-    if constexpr (H::kTileOcc > 0) {
-        if (a.order && a.tile_next) {  // bucketed ragged batch: persistent tile queue
-            auto kern = hmac ? md_tiles_kernel<H, true> : md_tiles_kernel<H, false>;
-            int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kTileWaves, 0) != hipSuccess || per_cu <= 0)
-                per_cu = 1;
-            per_cu = per_cu > kTileWgPerCu ? kTileWgPerCu : per_cu;
-            const uint64_t ntiles = (a.count + 63) / 64;
-            uint64_t grid = (uint64_t)per_cu * device_cu_count();
-            const uint64_t need = (ntiles + kTileWaves - 1) / kTileWaves;
-            if (grid > need) grid = need > 0 ? need : 1;
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * kTileWaves), 0, s, a,
-                               (uint32_t)(grid * kTileStreamWaves), (uint32_t)(grid * kTileWaves));
-            return;
-        }
+    if (a.order && a.tile_next) {  // bucketed ragged batch: persistent tile queue
+        if (hmac ? launch_tiles<H, kTileHmac>(a, s) : launch_tiles<H, kTilePlain>(a, s)) return;
     }
     if (a.count < kPfMaxCount) {
         if (hmac) hipLaunchKernelGGL((md_batch_kernel<H, true, true>), grid_for(a.count), dim3(256), 0, s, a);
@@ -461,6 +287,10 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
 
 template <class H>
 void launch_md_keyed(const KArgs& a, hipStream_t s) {
+    if (a.order && a.tile_next) {  // bucketed ragged batch: the tile kernel's keyed modes
+        if (a.key_mode == kKeyHmac && launch_tiles<H, kTileKeyedHmac>(a, s)) return;
+        if (a.key_mode == kKeySuffix && launch_tiles<H, kTileKeyedSuffix>(a, s)) return;
+    }
     switch (a.key_mode) {
     case kKeyHmac: hipLaunchKernelGGL((md_keyed_kernel<H, kKeyHmac>), grid_for(a.count), dim3(256), 0, s, a); break;
     case kKeyPrefix: hipLaunchKernelGGL((md_keyed_kernel<H, kKeyPrefix>), grid_for(a.count), dim3(256), 0, s, a); break;

@@ -1,0 +1,436 @@
+// md_tiles.hpp — the persistent tile kernel of bucketed ragged MD-family
+// batches (64-byte-block hashes: MD5), included by md_kernels.hpp.
+//
+// A length-bucketed batch (lcb_kernels.hip launch_bucketing: `order` lists
+// messages by key = length class x start phase, longest class first, every
+// key's run padded to whole tiles for a large batch) is cut into TILES of 64
+// consecutive `order` entries; one wave hashes one tile at a time, lane =
+// message.  Workgroups of 4 waves, 5 per CU (each wave owns an 8 KiB LDS
+// slab: the whole 160 KiB), at most 96 VGPRs.  Every wave's first tile is
+// static (its global wave id), later ones come from a device-scope atomic
+// queue head; every wave leaves once the queue is past the last tile, so the
+// grid drains.
+//
+// THE PHASE STREAM.  The records of a tile share their length class (their
+// 64-B block counts differ by at most one) and their start phase, so one
+// wave moves them through its slab by coalesced LDS-DMA as in the
+// fixed-stride kernel (GatherLineStream: 8 records x one 128-B line per
+// global_load_lds_dwordx4), from a 16-B aligned stream base, and shifts the
+// bytes into blocks in registers:
+//   phase 0 / 1 (16-B aligned record, first / second half of a 128-B line):
+//     the stream is the record's whole 128-B cache lines (base = start
+//     rounded down to 128 B), read once with the nt policy; block b is dword
+//     Q + 16 b of the stream, Q = 0 / 16;
+//   phase 2 + q (any other start): base = start rounded down to 16 B, Q = q
+//     = the start's dword inside its 16-B chunk (uniform in the tile), and
+//     the lane's own byte offset sh = start & 3 is one v_alignbyte per word
+//     (default cache policy: a 128-B stream line spans two cache lines, the
+//     second is still in L2 when the next line asks for it).
+// Block 2L is entirely in line L; block 2L - 1 needs the last 16 dwords of
+// line L - 1 (kept in VGPRs, `carry`) and dwords 0..Q of line L.  The stream
+// carries every byte of the record, the last partial line included: a DMA
+// chunk is issued only if it holds at least one byte of its record (a 16-B
+// aligned chunk never crosses a page), so no per-lane global load remains
+// and the tail, the 0x80 / length padding and the key bytes of a
+// secret-suffix message are assembled in registers from the streamed words.
+//
+// Tiles that mix phases (small unpadded batches only) take the per-lane
+// message loop (md_tile_direct).
+//
+// Modes (template kMode):
+//   kTilePlain      H(m)
+//   kTileHmac       HMAC(K, m), one key: mid-states at a.mid (md5.h:309-369)
+//   kTileKeyedHmac  HMAC(K_k, m), k = key_index[i] (lcb_hash_batch_keyed)
+//   kTileKeyedSuffix H(m || K_k) (radius.h:1315-1377, the packet authenticator)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "hash_device.hpp"
+#include "lcb_internal.hpp"
+
+namespace lcbgpu {
+
+enum { kTilePlain = 0, kTileHmac = 1, kTileKeyedHmac = 2, kTileKeyedSuffix = 3 };
+
+constexpr int kTileWaves = 4;     // waves per workgroup (one 8 KiB slab each)
+constexpr int kTileWgPerCu = 4;   // 4 waves per SIMD (kTileOcc): 128 KiB of LDS
+
+__device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
+    const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
+    return k < a.nkeys ? k : a.nkeys - 1;   // never out of range: lcb_hash_batch_keyed checked the indices
+}
+
+// One lane's record of a tile.  A pad entry (kOrderPad) takes lane 0's
+// record (never a pad) so every DMA address stays inside the batch; its
+// digest is not stored.
+struct TileRec {
+    const uint8_t* p;
+    uint32_t idx;
+    uint32_t len;
+    bool valid;
+};
+
+// The next tile, claimed near the end of the current one in three steps, one
+// per stream line, so the dependent round trips (queue atomic -> order entry
+// -> offset / length) are waited for by the line stream's own waits.
+struct TileClaim {
+    uint64_t t;      // tile (wave-uniform)
+    uint32_t ent;    // this lane's order entry
+    TileRec r;
+    int stage;       // 0: nothing yet, 1: t, 2: ent, 3: r
+};
+
+__device__ __forceinline__ void tile_rec_load(const KArgs& a, uint32_t ent, TileRec& r) {
+    r.valid = ent != kOrderPad;
+    const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane(ent);
+    r.idx = r.valid ? ent : e0;
+    r.p = gptr(a.data) + (a.offsets ? gptr(a.offsets)[r.idx] : (uint64_t)r.idx * a.stride);
+    r.len = a.lengths ? gptr(a.lengths)[r.idx] : a.fixed_len;
+}
+
+__device__ __forceinline__ uint32_t tile_entry(const KArgs& a, uint64_t t, uint32_t lane, uint32_t norder) {
+    const uint64_t i = t * 64 + lane;
+    return i < norder ? gptr(a.order)[i] : kOrderPad;
+}
+
+// One step of the claim.  nwaves: first queue ticket = the static tiles.
+__device__ __forceinline__ void tile_claim_step(const KArgs& a, TileClaim& c, uint32_t lane, uint64_t ntiles,
+                                                uint32_t norder, uint32_t nwaves) {
+    if (c.stage == 0) {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(a.tile_next, 1u);   // device scope, returns the old head
+        c.t = (uint64_t)nwaves + (uint32_t)__builtin_amdgcn_readfirstlane(v);
+    } else if (c.stage == 1) {
+        if (c.t < ntiles) c.ent = tile_entry(a, c.t, lane, norder);
+    } else if (c.stage == 2) {
+        if (c.t < ntiles) tile_rec_load(a, c.ent, c.r);
+    }
+    ++c.stage;
+}
+
+// Message geometry / key of a lane for the tile modes.
+template <class H, int kMode>
+struct TileMsg {
+    uint64_t total;     // bytes hashed after the state's prefix (message [+ suffix key])
+    uint64_t prefix;    // bytes already in the state (HMAC: one block)
+    const uint8_t* K;   // suffix key
+    uint32_t kl;
+};
+
+// One block from the stream window X = c[0..15] ++ y[0..15] (c: dwords
+// 16..31 of line L - 1, y: dwords 0..15 of line L, for block 2L - 1; c = y =
+// line L for block 2L): X[Q + k] byte-shifted by sh, k = 0..15, i.e. the 16
+// raw LE words of the block (Q = 16: X[16..31] as they are).
+template <int Q>
+__device__ __forceinline__ void tile_shift(const uint32_t* c, const uint32_t* y, uint32_t sh, uint32_t w[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int j = Q + k;
+        if (Q == 16) {
+            w[k] = y[k];
+        } else {
+            const uint32_t lo = j < 16 ? c[j] : y[j - 16];
+            const uint32_t hi = j + 1 < 16 ? c[j + 1] : y[j + 1 - 16];
+            w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+    }
+}
+// Dispatch on the tile's (wave-uniform) Q.  Q passes through an empty asm at
+// every call so the compiler does not clone the whole line loop per Q.
+__device__ __forceinline__ void tile_assemble(uint32_t Q, const uint32_t* c, const uint32_t* y, uint32_t sh,
+                                              uint32_t w[16]) {
+    asm volatile("" : "+s"(Q));
+    switch (Q) {
+    case 0: tile_shift<0>(c, y, sh, w); break;
+    case 1: tile_shift<1>(c, y, sh, w); break;
+    case 2: tile_shift<2>(c, y, sh, w); break;
+    case 3: tile_shift<3>(c, y, sh, w); break;
+    default: tile_shift<16>(c, y, sh, w); break;
+    }
+}
+
+// Compression inside the tile kernel: MD5 with its T constants as inline
+// literals (Md5::addk), other hashes as they are.
+template <class H>
+__device__ __forceinline__ void tile_compress(H& st, const uint32_t* w) {
+    if constexpr (std::is_same<H, Md5>::value) st.template compress<true>(w);
+    else st.compress(w);
+}
+
+// Block b of a lane's (virtual) message from the streamed words w: whole
+// message blocks go straight to compress; the block holding the message's
+// end gets its bytes past the end cleared, the suffix key's bytes (keyed
+// suffix), the 0x80 terminator and, in the last block, the bit length of
+// prefix + total (md5.h:266-288).  Lanes whose message has fewer blocks do
+// nothing.  nfull_min: wave minimum of whole message blocks (uniform fast path).
+template <class H, int kMode>
+__device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint64_t len, const TileMsg<H, kMode>& m,
+                                           uint32_t nblk, uint32_t nfull_min) {
+    if (b < nfull_min) {           // wave-uniform: every lane has a whole message block here
+        tile_compress(st, w);
+        return;
+    }
+    if (b >= nblk) return;         // this lane is done
+    const uint64_t pos = (uint64_t)b * 64;
+    if (pos + 64 > len) {          // the block holds the end of the message
+        const int rb = pos >= len ? 0 : (int)(len - pos);   // message bytes in the block
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int v = rb - 4 * k;
+            w[k] &= v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu >> (32 - 8 * v)));
+        }
+        if (kMode == kTileKeyedSuffix) {
+            const uint64_t e = pos + 64 < m.total ? pos + 64 : m.total;   // key bytes [max(pos, len), e)
+            const uint64_t s0 = pos > len ? pos : len;
+            if (s0 < e) or_window64(m.K + pos - len, (uint32_t)(s0 - pos), (uint32_t)(e - pos), w);
+        }
+        if (m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
+        if (b + 1 == nblk) H::put_length(w, m.total + m.prefix);
+    }
+    tile_compress(st, w);
+}
+
+template <class H, int kMode>
+__device__ __forceinline__ void tile_finish(const KArgs& a, H& st, const TileRec& r) {
+    uint32_t dw[H::kDigest / 4];
+    st.digest_words(dw);
+    if (kMode == kTileHmac || kMode == kTileKeyedHmac) {
+        const uint32_t* mid = gptr(a.mid);
+        if (kMode == kTileKeyedHmac) mid += (uint64_t)key_of(a, r.idx) * 2 * kMidWords;
+        H o;
+        load_words(o.s, mid + kMidWords);   // state after K ^ opad
+        md_outer(o, dw);
+        o.digest_words(dw);
+    }
+    if (r.valid) store_digest<H::kDigest>(a.digests + (uint64_t)r.idx * H::kDigest, dw);
+}
+
+template <class H, int kMode>
+__device__ __forceinline__ void tile_state(const KArgs& a, const TileRec& r, H& st, TileMsg<H, kMode>& m) {
+    m.prefix = 0;
+    m.total = r.len;
+    m.K = nullptr;
+    m.kl = 0;
+    if (kMode == kTileHmac || kMode == kTileKeyedHmac) {
+        const uint32_t* mid = gptr(a.mid);
+        if (kMode == kTileKeyedHmac) mid += (uint64_t)key_of(a, r.idx) * 2 * kMidWords;
+        load_words(st.s, mid);              // state after K ^ ipad
+        m.prefix = H::kBlock;
+    } else {
+        st.init();
+    }
+    if (kMode == kTileKeyedSuffix) {
+        const uint32_t k = key_of(a, r.idx);
+        m.K = gptr(a.keys) + gptr(a.key_off)[k];
+        m.kl = gptr(a.key_len)[k];
+        m.total += m.kl;
+    }
+}
+
+// Per-lane message loop for a tile whose records do not share a phase.
+template <class H, int kMode>
+__device__ __forceinline__ void md_tile_direct(const KArgs& a, const TileRec& r) {
+    H st;
+    TileMsg<H, kMode> m;
+    tile_state(a, r, st, m);
+    if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m.K, m.kl, 0);
+    else md_message(st, r.p, r.len, m.prefix);
+    tile_finish<H, kMode>(a, st, r);
+}
+
+// The tile's line stream: lane l owns record l.  Line L of the 64 records
+// moves into the wave's 8 KiB slab with 8 global_load_lds_dwordx4, instruction
+// g carrying chunk g (bytes 16 g .. 16 g + 15) of every record's line, so
+// slot (g, l) = slab + 1024 g + 16 l, and lane l reads its line back with 8
+// conflict-free ds_read_b128 (16 consecutive lanes read 256 contiguous bytes).
+// Per lane: one 64-bit line address (2 VGPRs; the 8 chunk addresses are
+// formed at issue), against 8 per-lane record pointers (16 VGPRs) in the
+// fixed kernel's 8-records-per-instruction layout.  A chunk that holds no
+// byte of the lane's record (the last lines of a tile) is fetched from the
+// record's first chunk instead: same page, never used.
+struct LaneLineStream {
+    uint8_t* slab;
+    const uint8_t* line;   // this lane's record, current line
+    __device__ __forceinline__ void init(const uint8_t* base, uint8_t* my_slab) {
+        slab = my_slab;
+        line = base;
+    }
+    template <int kAux>
+    __device__ __forceinline__ void issue(uint32_t L, bool masked, uint64_t end, const uint8_t* base) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint8_t* src = line + 16 * g;
+            if (masked) src = (uint64_t)L * 128u + 16u * g < end ? src : base;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
+        }
+        line += 128;
+    }
+    // Waits for the issued line and copies this lane's 128 B (raw LE words).
+    __device__ __forceinline__ void take(uint32_t y[32], uint32_t lane) const {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        using lds_cu4 = __attribute__((address_space(3))) const v4u;
+        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) + lane * 16;
+        asm volatile("" : "+v"(b));
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const v4u v = *(lds_cu4*)(uintptr_t)(b + (uint32_t)(g * 1024));
+            y[4 * g] = v.x; y[4 * g + 1] = v.y; y[4 * g + 2] = v.z; y[4 * g + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab free again
+    }
+};
+
+template <class H, int kMode>
+__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
+                                               uint32_t Q, bool whole_lines, TileClaim& cl, uint64_t ntiles,
+                                               uint32_t norder, uint32_t nwaves) {
+    const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
+    const uint32_t sh = p32 & 3u;
+    // Stream offset of the record's first byte: base = p - off0.
+    const uint32_t off0 = Q == 16 ? 64u : (p32 & 15u);
+    const uint64_t len = r.len;
+    H st;
+    TileMsg<H, kMode> m;
+    tile_state(a, r, st, m);
+    // Geometry: lines holding record bytes, lines wholly inside every record,
+    // blocks of the padded (virtual) message, whole message blocks.
+    const uint64_t end = off0 + len;                        // record end, in stream bytes
+    const uint32_t nblk = (uint32_t)((m.total + 8u) >> 6) + 1u;
+    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7), NB = nblk, NF = r.len >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {                       // wave max / min (xor butterfly)
+        NL = max(NL, (uint32_t)__shfl_xor((int)NL, d, 64));
+        NB = max(NB, (uint32_t)__shfl_xor((int)NB, d, 64));
+        NS = min(NS, (uint32_t)__shfl_xor((int)NS, d, 64));
+        NF = min(NF, (uint32_t)__shfl_xor((int)NF, d, 64));
+    }
+    NL = __builtin_amdgcn_readfirstlane(NL);
+    NB = __builtin_amdgcn_readfirstlane(NB);
+    NS = __builtin_amdgcn_readfirstlane(NS);
+    NF = __builtin_amdgcn_readfirstlane(NF);
+    const uint8_t* base = r.p - off0;
+    LaneLineStream ls;
+    ls.init(base, slab);
+    auto issue = [&](uint32_t L) {
+        const bool masked = L >= NS;
+        if (whole_lines) ls.issue<kLdsAux>(L, masked, end, base);
+        else ls.issue<kGatherAux>(L, masked, end, base);
+    };
+    const uint32_t c0 = NL > 3 ? NL - 3 : 0u;                // first claim step
+    if (NL) issue(0);
+    uint32_t c[16];   // dwords 16..31 of the previous line (the carry)
+    // Whole-block lines: both blocks of line L (2L - 1 and 2L) are whole
+    // message blocks of every lane (2L < NF).
+    const uint32_t LF = (NF + 1) / 2 < NL ? (NF + 1) / 2 : NL;
+    uint32_t L = 0;
+    for (; L < LF; ++L) {
+        uint32_t y[32];
+        ls.take(y, lane);
+        if (L + 1 < NL) issue(L + 1);
+        if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
+        uint32_t w[16];
+        if (L > 0) {   // block 2L - 1: the carry and dwords 0..Q of this line
+            tile_assemble(Q, c, y, sh, w);
+            tile_compress(st, w);
+        }
+        tile_assemble(Q, y, y + 16, sh, w);   // block 2L: dwords Q..Q+16 of this line
+        tile_compress(st, w);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+    }
+    // The rest, one block per step (tile_block: ends of messages, padding,
+    // length, suffix key bytes).  Block b = 2L - 1 takes line L (zeros past
+    // the last line: those bytes lie past every record's end) and assembles
+    // block 2L from it at once, kept in `wn` (16 VGPRs, not the whole line)
+    // for the next step.
+    uint32_t wn[16];
+    for (uint32_t b = LF ? 2 * LF - 1 : 0; b < NB; ++b) {
+        uint32_t w[16];
+        if ((b & 1) || b == 0) {        // wave-uniform
+            uint32_t y[32];
+            L = (b + 1) >> 1;
+            if (L < NL) {
+                ls.take(y, lane);
+                if (L + 1 < NL) issue(L + 1);
+                if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 32; ++k) y[k] = 0u;
+            }
+            if (b & 1) {
+                tile_assemble(Q, c, y, sh, w);
+                tile_assemble(Q, y, y + 16, sh, wn);
+            } else {                    // b == 0
+                tile_assemble(Q, y, y + 16, sh, w);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = wn[k];
+        }
+        tile_block<H, kMode>(st, b, w, len, m, nblk, NF);
+    }
+    tile_finish<H, kMode>(a, st, r);
+}
+
+template <class H, int kMode>
+__global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nwaves) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kTileWaves][8192];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
+    const uint64_t ntiles = (norder + 63) / 64;
+    TileClaim cl;
+    cl.t = (uint64_t)blockIdx.x * kTileWaves + wv;   // first tile: static
+    cl.stage = 3;
+    if (cl.t < ntiles) tile_rec_load(a, tile_entry(a, cl.t, lane, norder), cl.r);
+    while (cl.t < ntiles) {
+        const TileRec r = cl.r;
+        cl.stage = 0;
+        // The tile's phase: Q (uniform) or a mixed tile.
+        // Q: 16 for a record on the second half of a 128-B line, 0 on its
+        // first half (both: the stream is whole cache lines), else the
+        // start's dword inside its 16-B chunk.
+        const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
+        const bool wl = (p32 & 63u) == 0;
+        const uint32_t Ql = wl ? ((p32 & 64u) ? 16u : 0u) : ((p32 >> 2) & 3u);
+        const uint32_t Q = (uint32_t)__builtin_amdgcn_readfirstlane(Ql);
+        if (__all(Ql == Q)) {
+            md_tile_stream<H, kMode>(a, r, lane, &slab[wv][0], Q, __all(wl), cl, ntiles, norder, nwaves);
+        } else {
+            md_tile_direct<H, kMode>(a, r);
+        }
+        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
+    }
+}
+
+// Launch of the tile kernel on a bucketed batch (a.order, a.tile_next set);
+// false if this hash has no tile kernel.
+template <class H, int kMode>
+__host__ bool launch_tiles(const KArgs& a, hipStream_t s) {
+    if constexpr (H::kTileOcc > 0) {
+        auto kern = md_tiles_kernel<H, kMode>;
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kTileWaves, 0) != hipSuccess || per_cu <= 0)
+            per_cu = 1;
+        per_cu = per_cu > kTileWgPerCu ? kTileWgPerCu : per_cu;
+        // Upper bound of the tile count (the device knows the exact one).
+        const uint64_t ntiles = (a.count + 63) / 64 + kBucketKeys;
+        uint64_t grid = (uint64_t)per_cu * device_cu_count();
+        const uint64_t need = (ntiles + kTileWaves - 1) / kTileWaves;
+        if (grid > need) grid = need > 0 ? need : 1;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * kTileWaves), 0, s, a,
+                           (uint32_t)(grid * kTileWaves));
+        return true;
+    } else {
+        (void)a;
+        (void)s;
+        return false;
+    }
+}
+
+}  // namespace lcbgpu

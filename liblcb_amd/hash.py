@@ -89,6 +89,70 @@ def _check_extent(nbytes, count, offsets, lengths, stride, fixed_len):
         raise ValueError("messages extend to byte %d of a %d-byte buffer" % (end, nbytes))
 
 
+def _dev_batch(data, count, offsets, lengths, stride, fixed_len, out, D, per_msg=()):
+    """Validate a device-mode batch description and return (count, stride,
+    fixed_len, out): data uint8 and contiguous; offsets int64/uint64 and
+    lengths int32/uint32 (the C-ABI reads them as uint64 / uint32), per-message
+    uint32 arrays (`per_msg`: (name, tensor) pairs, e.g. key_index) int32 /
+    uint32, all contiguous, on data's device and with >= count entries;
+    `out` (allocated if None) uint8, contiguous, on data's device, >= count x D
+    bytes; every message inside data (_check_extent)."""
+    if data.dtype != torch.uint8 or not data.is_contiguous():
+        raise TypeError("data must be a contiguous uint8 tensor")
+    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
+    for name, t, dts in (("offsets", offsets, (torch.int64, torch.uint64)),
+                         ("lengths", lengths, (torch.int32, torch.uint32))) + \
+            tuple((n, t, (torch.int32, torch.uint32)) for n, t in per_msg):
+        if t is None:
+            continue
+        if not _is_dev(t) or t.device != data.device:
+            raise ValueError("%s must be a tensor on %s" % (name, data.device))
+        if t.dtype not in dts or not t.is_contiguous():
+            raise TypeError("%s must be a contiguous %s tensor" % (name, " / ".join(str(d) for d in dts)))
+        if int(t.numel()) < count:
+            raise ValueError("%s has %d entries, count is %d" % (name, int(t.numel()), count))
+    _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
+    if out is None:
+        out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+    elif not _is_dev(out) or out.device != data.device or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise TypeError("out must be a contiguous uint8 tensor on %s" % data.device)
+    if int(out.numel()) < count * D:
+        raise ValueError("out holds %d bytes, %d x %d needed" % (int(out.numel()), count, D))
+    return count, stride, fixed_len, out
+
+
+def _host_batch(data, count, offsets, lengths, stride, fixed_len, out, D, per_msg=()):
+    """Host-mode counterpart of _dev_batch: -> (data, offsets, lengths,
+    per_msg arrays, count, stride, fixed_len, out, nbytes) as contiguous
+    numpy arrays of the dtypes the C-ABI reads."""
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        data = np.frombuffer(bytes(data), dtype=np.uint8)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    nbytes = data.size
+    if data.size == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if lengths is not None:
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
+    arrs = []
+    for name, t in per_msg:
+        if t is not None:
+            t = np.ascontiguousarray(t, dtype=np.uint32)
+            if t.size < count:
+                raise ValueError("%s has %d entries, count is %d" % (name, t.size, count))
+        arrs.append(t)
+    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
+    if out is None:
+        out = np.empty((count, D), dtype=np.uint8)
+    elif not isinstance(out, np.ndarray) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+        raise TypeError("out must be a C-contiguous uint8 numpy array")
+    if out.size < count * D:
+        raise ValueError("out holds %d bytes, %d x %d needed" % (out.size, count, D))
+    return data, offsets, lengths, arrs, count, stride, fixed_len, out, nbytes
+
+
 def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None,
                fixed_len=None, key=None, out=None):
     """Digest (or HMAC when `key` is given) of every message of a batch.
@@ -108,15 +172,7 @@ def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None
     klen = len(kb) if kb is not None else 0
     L = lib()
     if _is_dev(data):
-        assert data.dtype == torch.uint8 and data.is_contiguous()
-        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
-        for t, dt in ((offsets, (torch.int64, torch.uint64)), (lengths, (torch.int32, torch.uint32))):
-            if t is not None:
-                assert _is_dev(t) and t.dtype in dt and t.is_contiguous() and t.device == data.device
-        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
-        if out is None:
-            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
-        assert out.numel() >= count * D
+        count, stride, fixed_len, out = _dev_batch(data, count, offsets, lengths, stride, fixed_len, out, D)
         with torch.cuda.device(data.device):
             stream = torch.cuda.current_stream(data.device).cuda_stream
             check(L.lcb_hash_batch(alg, kptr, klen, data.data_ptr(),
@@ -124,22 +180,8 @@ def hash_batch(alg, data, *, offsets=None, lengths=None, count=None, stride=None
                                    lengths.data_ptr() if lengths is not None else None,
                                    count, stride, fixed_len, out.data_ptr(), F_DEVICE, stream))
         return out
-    # host mode
-    if isinstance(data, (bytes, bytearray, memoryview)):
-        data = np.frombuffer(bytes(data), dtype=np.uint8)
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    nbytes = data.size
-    if data.size == 0:
-        data = np.zeros(1, dtype=np.uint8)
-    if offsets is not None:
-        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-    if lengths is not None:
-        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
-    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
-    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
-    if out is None:
-        out = np.empty((count, D), dtype=np.uint8)
-    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= count * D
+    data, offsets, lengths, _, count, stride, fixed_len, out, _ = _host_batch(
+        data, count, offsets, lengths, stride, fixed_len, out, D)
     check(L.lcb_hash_batch(alg, kptr, klen, data.ctypes.data,
                            offsets.ctypes.data if offsets is not None else None,
                            lengths.ctypes.data if lengths is not None else None,
@@ -224,7 +266,9 @@ def hash_batch_multi(devs, alg, data, *, offsets=None, lengths=None, count=None,
                      fixed_len=None, key=None, out=None, copy_parts=False):
     """lcb_hash_batch_multi: the batch split by `partition` over the HIP
     devices `devs` (repeats allowed) and hashed on all of them at once.
-    Device tensors must live on devs[0]; numpy input runs in host mode."""
+    Device tensors must live on devs[0]; the call is ordered after torch's
+    current stream on devs[0] (passed as the ABI's `stream`).  numpy input
+    runs in host mode."""
     if isinstance(alg, str):
         alg = ALG_IDS[alg]
     D = DIGEST_SIZE[alg]
@@ -233,35 +277,24 @@ def hash_batch_multi(devs, alg, data, *, offsets=None, lengths=None, count=None,
     klen = len(kb) if kb is not None else 0
     dv = (ctypes.c_int * len(devs))(*devs)
     if _is_dev(data):
-        assert data.dtype == torch.uint8 and data.is_contiguous() and data.device.index == devs[0]
-        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
-        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
-        if out is None:
-            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
-        torch.cuda.synchronize(data.device)     # inputs written on torch's stream are complete
+        if data.device.index != devs[0]:
+            raise ValueError("device tensors must live on devs[0] = %d" % devs[0])
+        count, stride, fixed_len, out = _dev_batch(data, count, offsets, lengths, stride, fixed_len, out, D)
+        stream = torch.cuda.current_stream(data.device).cuda_stream
         check(lib().lcb_hash_batch_multi(dv, len(devs), alg, kptr, klen, data.data_ptr(),
                                          offsets.data_ptr() if offsets is not None else None,
                                          lengths.data_ptr() if lengths is not None else None,
                                          count, stride, fixed_len, out.data_ptr(),
-                                         F_DEVICE | (F_COPY_PARTS if copy_parts else 0)))
+                                         F_DEVICE | (F_COPY_PARTS if copy_parts else 0), stream))
         return out
-    data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8)
-                                if isinstance(data, (bytes, bytearray, memoryview)) else data, dtype=np.uint8)
-    nbytes = data.size
-    if data.size == 0:
-        data = np.zeros(1, dtype=np.uint8)
-    if offsets is not None:
-        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-    if lengths is not None:
-        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
-    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
-    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
-    if out is None:
-        out = np.empty((count, D), dtype=np.uint8)
+    if copy_parts:
+        raise ValueError("copy_parts is a device-mode option")
+    data, offsets, lengths, _, count, stride, fixed_len, out, _ = _host_batch(
+        data, count, offsets, lengths, stride, fixed_len, out, D)
     check(lib().lcb_hash_batch_multi(dv, len(devs), alg, kptr, klen, data.ctypes.data,
                                      offsets.ctypes.data if offsets is not None else None,
                                      lengths.ctypes.data if lengths is not None else None,
-                                     count, stride, fixed_len, out.ctypes.data, 0))
+                                     count, stride, fixed_len, out.ctypes.data, 0, None))
     return out
 
 
@@ -283,14 +316,8 @@ def hash_batch_keyed(alg, mode, keys, data, *, key_index=None, offsets=None, len
         koff[1:] = np.cumsum(klen[:-1], dtype=np.uint64)
     L = lib()
     if _is_dev(data):
-        assert data.dtype == torch.uint8 and data.is_contiguous()
-        count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.numel())
-        _check_extent(data.numel(), count, offsets, lengths, stride, fixed_len)
-        if key_index is not None:
-            assert _is_dev(key_index) and key_index.dtype in (torch.int32, torch.uint32) and \
-                key_index.numel() >= count and key_index.is_contiguous()
-        if out is None:
-            out = torch.empty((count, D), dtype=torch.uint8, device=data.device)
+        count, stride, fixed_len, out = _dev_batch(data, count, offsets, lengths, stride, fixed_len, out, D,
+                                                   per_msg=(("key_index", key_index),))
         with torch.cuda.device(data.device):
             stream = torch.cuda.current_stream(data.device).cuda_stream
             check(L.lcb_hash_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data,
@@ -299,23 +326,8 @@ def hash_batch_keyed(alg, mode, keys, data, *, key_index=None, offsets=None, len
                                          lengths.data_ptr() if lengths is not None else None,
                                          count, stride, fixed_len, out.data_ptr(), F_DEVICE, stream))
         return out
-    if isinstance(data, (bytes, bytearray, memoryview)):
-        data = np.frombuffer(bytes(data), dtype=np.uint8)
-    data = np.ascontiguousarray(data, dtype=np.uint8)
-    nbytes = data.size
-    if data.size == 0:
-        data = np.zeros(1, dtype=np.uint8)
-    if offsets is not None:
-        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-    if lengths is not None:
-        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
-    count, stride, fixed_len = _layout(count, offsets, lengths, stride, fixed_len, data.size)
-    _check_extent(nbytes, count, offsets, lengths, stride, fixed_len)
-    if key_index is not None:
-        key_index = np.ascontiguousarray(key_index, dtype=np.uint32)
-        assert key_index.size >= count
-    if out is None:
-        out = np.empty((count, D), dtype=np.uint8)
+    data, offsets, lengths, (key_index,), count, stride, fixed_len, out, _ = _host_batch(
+        data, count, offsets, lengths, stride, fixed_len, out, D, per_msg=(("key_index", key_index),))
     check(L.lcb_hash_batch_keyed(alg, mode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data, len(keys),
                                  key_index.ctypes.data if key_index is not None else None, data.ctypes.data,
                                  offsets.ctypes.data if offsets is not None else None,

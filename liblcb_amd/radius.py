@@ -43,7 +43,7 @@ RANDOM_AUTH = (ACCESS_REQUEST, STATUS_SERVER, STATUS_CLIENT)
 ZERO_AUTH = (ACCOUNTING_REQUEST, DISCONNECT_REQUEST, COA_REQUEST)
 REPLY_AUTH = (ACCESS_ACCEPT, ACCESS_REJECT, ACCESS_CHALLENGE, DISCONNECT_ACK, DISCONNECT_NAK, COA_ACK, COA_NAK)
 
-__all__ = ["radius_pkt_sign_batch", "radius_pkt_verify_batch", "find_attr"]
+__all__ = ["radius_pkt_sign_batch", "radius_pkt_verify_batch", "find_attr", "pkt_len"]
 
 
 def find_attr(pkt, attr_type):
@@ -58,6 +58,24 @@ def find_attr(pkt, attr_type):
             return i
         i += n
     return None
+
+
+def pkt_len(pkt):
+    """The packet's own Length field (RADIUS_PKT_HDR_LEN_GET, radius.h): the
+    reference hashes [0, Length) and ignores buffer bytes past it
+    (radius.h:913 RADIUS_PKT_END, :1333)."""
+    return int.from_bytes(pkt[2:4], "big")
+
+
+def _pw_check(n):
+    """radius_pkt_attr_password_encode's checks for a User-Password of n data
+    bytes encoded in place (radius.h:752-765): 0 or the error it returns."""
+    if n > 128:
+        return errno.EINVAL
+    aligned = ((n + 15) & ~15) if n else 16
+    if aligned > n:          # buf_size = n: not a nonzero multiple of 16
+        return errno.EOVERFLOW
+    return 0
 
 
 def _pack(msgs):
@@ -86,14 +104,21 @@ def _keyed(mode, keys, msgs, kidx, device):
     return [bytes(r) for r in d]
 
 
-def _password_encode(pkts, keys, key_index, device):
+def _password_encode(pkts, keys, key_index, err, device):
     """radius.h:745-790 on every packet's User-Password, in place: block j
-    of all packets in one KEY_PREFIX batch (the chain is serial per packet)."""
+    of all packets in one KEY_PREFIX batch (the chain is serial per packet).
+    A password the reference refuses (_pw_check) sets err[n] and leaves the
+    packet untouched, as radius_pkt_sign returns before writing."""
     jobs = []
     for n, p in enumerate(pkts):
         o = find_attr(p, ATTR_USER_PASSWORD)
-        if o is not None and p[o + 1] > 2:
-            jobs.append((n, o + 2, p[o + 1] - 2))
+        if o is None:
+            continue
+        e = _pw_check(p[o + 1] - 2)
+        if e:
+            err[n] = e
+            continue
+        jobs.append((n, o + 2, p[o + 1] - 2))
     prev = {n: bytes(pkts[n][4:20]) for n, _, _ in jobs}          # the authenticator
     j = 0
     while True:
@@ -113,30 +138,35 @@ def radius_pkt_sign_batch(packets, keys, key_index=None, device=False):
     """radius_pkt_sign(pkt, ..., key, key_len, add_msg_authr = 0) of every
     packet (radius.h:1487-1531): User-Password encoded, an existing
     Message-Authenticator and the authenticator updated with the packet's
-    authenticator inside.  packets: sequence of bytes (a reply already holds
-    its request's authenticator, radius_pkt_reply_init); keys: the shared
-    secrets; key_index[i]: packet i's secret (default 0).  Returns the
-    signed packets (bytes)."""
+    authenticator inside, each over the packet's [0, Length) only.  packets:
+    sequence of bytes (a reply already holds its request's authenticator,
+    radius_pkt_reply_init; bytes past Length are kept as they are); keys: the
+    shared secrets; key_index[i]: packet i's secret (default 0).  Returns
+    (errors, packets): errors[i] is 0 or the error radius_pkt_sign returns
+    (EINVAL / EOVERFLOW for a User-Password it refuses), and a failed packet
+    is returned unchanged."""
     n = len(packets)
     key_index = np.zeros(n, np.uint32) if key_index is None else np.asarray(key_index, np.uint32)
     pkts = [bytearray(p) for p in packets]
-    _password_encode(pkts, keys, key_index, device)
+    err = np.zeros(n, np.int64)
+    _password_encode(pkts, keys, key_index, err, device)
     # Message-Authenticator, authenticator inside (radius.h:866-872, 906-916):
     # HMAC over the packet with the attribute's 16 data bytes zeroed.
-    ma = [(i, find_attr(p, ATTR_MSG_AUTHENTIC)) for i, p in enumerate(pkts)]
+    ma = [(i, find_attr(p, ATTR_MSG_AUTHENTIC)) for i, p in enumerate(pkts) if not err[i]]
     ma = [(i, o) for i, o in ma if o is not None]
     msgs = []
     for i, o in ma:
         pkts[i][o + 2:o + 18] = bytes(16)
-        msgs.append(bytes(pkts[i]))
+        msgs.append(bytes(pkts[i][:pkt_len(pkts[i])]))
     for (i, o), d in zip(ma, _keyed(KEY_HMAC, keys, msgs, [key_index[i] for i, _ in ma], device)):
         pkts[i][o + 2:o + 18] = d
     # Authenticator, inside: MD5(packet || secret) except for the codes whose
     # authenticator is random (radius.h:1322-1336, 1404-1421).
-    au = [i for i, p in enumerate(pkts) if p[0] not in RANDOM_AUTH]
-    for i, d in zip(au, _keyed(KEY_SUFFIX, keys, [bytes(pkts[i]) for i in au], [key_index[i] for i in au], device)):
+    au = [i for i, p in enumerate(pkts) if not err[i] and p[0] not in RANDOM_AUTH]
+    for i, d in zip(au, _keyed(KEY_SUFFIX, keys, [bytes(pkts[i][:pkt_len(pkts[i])]) for i in au],
+                               [key_index[i] for i in au], device)):
         pkts[i][4:20] = d
-    return [bytes(p) for p in pkts]
+    return err, [bytes(p) if not err[i] else bytes(packets[i]) for i, p in enumerate(pkts)]
 
 
 def _ma_authenticator(code, req):
@@ -190,7 +220,7 @@ def radius_pkt_verify_batch(packets, keys, key_index=None, requests=None, device
         if isinstance(a, int):
             err[i] = a
             continue
-        q = bytearray(p)
+        q = bytearray(p[:pkt_len(p)])
         if a is not None:
             q[4:20] = a
         q[o + 2:o + 18] = bytes(16)
@@ -208,7 +238,7 @@ def radius_pkt_verify_batch(packets, keys, key_index=None, requests=None, device
         if isinstance(a, int):
             err[i] = a
             continue
-        q = bytearray(p)
+        q = bytearray(p[:pkt_len(p)])
         q[4:20] = a
         jobs.append(i)
         msgs.append(bytes(q))

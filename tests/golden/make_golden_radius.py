@@ -54,6 +54,7 @@ def lib():
     L.ref_rad_authenticator_calc.argtypes = [u8p, sz, u8p, sz, ctypes.c_int, u8p, ctypes.c_void_p]
     L.ref_rad_msg_authenticator_calc.argtypes = [u8p, sz, u8p, sz, ctypes.c_int, u8p, ctypes.c_void_p]
     L.ref_rad_password_encode.argtypes = [u8p, u8p, sz, u8p, sz, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+    L.ref_rad_sign.argtypes = [u8p, sz, u8p, sz, ctypes.c_void_p, ctypes.POINTER(sz)]
     return L
 
 
@@ -147,5 +148,44 @@ def main():
                                                skipped))
 
 
+def edge():
+    """tests/golden/radius_edge.json: radius_pkt_sign (ref_rad_sign) on
+    (a) signed-able packets followed by bytes past their Length field (a
+    receive buffer longer than the packet: the reference hashes [0, Length)),
+    (b) Access-Requests whose User-Password data is 0, unaligned or over 128
+    bytes long (radius_pkt_attr_password_encode refuses them,
+    radius.h:752-765, and radius_pkt_sign returns that error)."""
+    L = lib()
+    rad = json.load(open(os.path.join(HERE, "radius.json")))
+    rng = np.random.default_rng(1315)
+    out = ctypes.create_string_buffer(4096)
+    ol = ctypes.c_size_t()
+    cases = []
+    for p in rad["packets"][:120]:
+        pre = bytes.fromhex(p["pre"])
+        tail = rng.integers(0, 256, int(rng.integers(1, 200)), dtype=np.uint8).tobytes()
+        k = p["key"]
+        rc = L.ref_rad_sign(pre + tail, len(pre) + len(tail), SECRETS[k], len(SECRETS[k]), out, ctypes.byref(ol))
+        cases.append({"what": "trailing", "key": k, "pre": (pre + tail).hex(), "rc": rc,
+                      "signed": out.raw[:ol.value].hex() if rc == 0 else None})
+    for n in (0, 1, 5, 15, 17, 33, 129, 130, 144, 160):
+        k = n % len(SECRETS)
+        auth = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        user = b"\x01\x06user"
+        attr = bytes([2, 2 + n]) + rng.integers(0x21, 0x7F, n, dtype=np.uint8).tobytes()
+        body = user + attr
+        hdr = bytes([1, int(rng.integers(0, 256))]) + (20 + len(body)).to_bytes(2, "big") + auth
+        pkt = hdr + body
+        rc = L.ref_rad_sign(pkt, len(pkt), SECRETS[k], len(SECRETS[k]), out, ctypes.byref(ol))
+        cases.append({"what": "password_len_%d" % n, "key": k, "pre": pkt.hex(), "rc": rc,
+                      "signed": out.raw[:ol.value].hex() if rc == 0 else None})
+    json.dump({"source": "reference radius_pkt_sign (oracle/ref_radius.c ref_rad_sign)", "cases": cases},
+              open(os.path.join(HERE, "radius_edge.json"), "w"), indent=0)
+    print("radius_edge.json: %d cases, rcs %s" % (len(cases), sorted({c["rc"] for c in cases})))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--edge":
+        edge()
+    else:
+        main()

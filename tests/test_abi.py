@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(L):
 
 
 def test_info_calls(L):
-    assert L.lcb_hash_gpu_abi_version() == 3
+    assert L.lcb_hash_gpu_abi_version() == 4
     assert [L.lcb_hash_digest_size(a) for a in range(0, 10)] == [0, 16, 20, 28, 32, 48, 64, 32, 64, 0]
     assert [L.lcb_hash_block_size(a) for a in range(1, 9)] == [64, 64, 64, 64, 128, 128, 64, 64]
     assert L.lcb_hash_strerror(errno.EINVAL) == b"invalid argument"

@@ -23,3 +23,18 @@ def test_c_caller_batches_equal_dropin_single_message(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK 3000 "), r.stdout
+
+
+def test_c_caller_multi_stream_contract(tmp_path):
+    """lcb_hash_batch_multi (ABI v4) ordered after the caller's stream:
+    tests/c/multi_stream.c writes the batch asynchronously on a non-default
+    stream and calls with no host sync; digests equal md5.h's."""
+    exe = str(tmp_path / "multi_stream")
+    subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", "-Wno-unused-function", "-D__HIP_PLATFORM_AMD__",
+                           "-I" + os.path.join(ROOT, "include"), "-I/opt/rocm/include", "-o", exe,
+                           os.path.join(ROOT, "tests", "c", "multi_stream.c"),
+                           "-L" + LIBDIR, "-llcb_hash_gpu", "-Wl,-rpath," + LIBDIR,
+                           "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK 65536"), r.stdout
