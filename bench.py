@@ -78,6 +78,10 @@ def parse(argv=None):
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--plan", action="store_true",
                    help="print every rank's shard (gloo, no GPU use) and exit: launch-path check")
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="process group of the N>1 ranks: nccl (= RCCL over xGMI, one rank per GPU) or gloo "
+                        "(timing barrier, max and digest gather on host tensors; ranks share devices "
+                        "round-robin, so --gpus 2 runs on a one-GPU box)")
     return p.parse_args(argv)
 
 
@@ -115,6 +119,15 @@ def shard_bounds(rank, world, per_gpu, scaling="weak", global_count_strong=None)
     total = global_count(scaling, world, per_gpu, global_count_strong)
     first = liblcb_amd.partition(world, count=total, fixed_len=MSG_LEN)
     return int(first[rank]), int(first[rank + 1] - first[rank])
+
+
+def all_shards(rank, world, first, count):
+    """[(first, count)] of every rank (gathered as objects: the launch check)."""
+    if world == 1:
+        return [[first, count]]
+    allp = [None] * world
+    dist.all_gather_object(allp, [first, count])
+    return allp
 
 
 def max_over_ranks(t, world):
@@ -318,17 +331,20 @@ def cpu_baseline(alg, count, threads):
 
 
 def cpu_per_alg(data, threads, best):
-    """Reference CPU rate of every algorithm on a bounded sample of the same
-    bytes (about 0.3 s wall each), the build `best` picked for the headline."""
+    """Reference CPU rate of every algorithm measured exactly as the headline
+    cpu_baseline: whole passes over the full workload (all buffers, one
+    contiguous shard per thread), repeated for >= 0.3 s wall, the build
+    `best` picked for the headline.  (Round 2 timed 64K-buffer samples, so
+    the threads' start-up was in every pass and the rates read ~1.5x low.)"""
     from oracle.pyoracle import REF_SIMD_SO, REF_SO, Ref
     path = {"reference": REF_SO, "reference-simd": REF_SIMD_SO}.get(best)
     if not path or not os.path.exists(path):
         return {}
     r = Ref(path)
     out = {}
+    n = len(data) // MSG_LEN
     for name, aid in sorted(ALG_IDS.items(), key=lambda x: x[1]):
-        n = min(len(data) // MSG_LEN, 1 << 16)
-        rate, t, _, reps = _ref_rate(r, aid, data, n, threads, 0.3)   # repeated for >= 0.3 s
+        rate, t, _, reps = _ref_rate(r, aid, data, n, threads, 0.3)
         out[name] = {"GiB_s": round(rate, 3), "buffers": n * reps, "threads": threads, "seconds": round(t, 3)}
     return out
 
@@ -385,8 +401,10 @@ def gather_digests(digests, first, n, total, world, rank):
         return digests.cpu().numpy(), 0.0
     first_all = liblcb_amd.partition(world, count=total, fixed_len=MSG_LEN)
     mx = int(np.max(np.diff(first_all.astype(np.int64))))
-    buf = torch.zeros((mx, D), dtype=torch.uint8, device="cuda")
-    buf[:n] = digests
+    # RCCL gathers device tensors; gloo gathers host tensors.
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    buf = torch.zeros((mx, D), dtype=torch.uint8, device=dev)
+    buf[:n] = digests.to(dev)
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
     torch.cuda.synchronize()
     dist.barrier()
@@ -658,8 +676,14 @@ def main():
     if a.plan:
         return plan(a, world, rank)
     if world > 1:
+        # One rank per GPU (LOCAL_RANK); with gloo more ranks than GPUs share
+        # them round-robin (device_count() does not initialise the GPU).
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
     else:
         torch.cuda.set_device(0)
@@ -686,6 +710,8 @@ def main():
         "unit": "GiB/s",
         "n_gpus": world,
         "world_size": dist.get_world_size() if world > 1 else 1,
+        "dist_backend": a.dist_backend if world > 1 else None,
+        "shards": all_shards(rank, world, first, count),
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(t / a.steps * 1e3, 4),
@@ -724,7 +750,8 @@ def main():
         if rank == 0:
             ok = verify_job(alg, allg, total)
             got = hashlib.sha256(allg.tobytes()).hexdigest()
-            out["gather"] = {"ms": round(gms, 3), "bytes": int(allg.nbytes), "collective": "gather (RCCL)"
+            out["gather"] = {"ms": round(gms, 3), "bytes": int(allg.nbytes),
+                             "collective": ("gather (%s)" % ("RCCL" if a.dist_backend == "nccl" else "gloo"))
                              if world > 1 else "none (1 rank)"}
             out.setdefault("verify", {})["job_digests_equal_reference"] = ok
             out["verify"]["digest_of_digests"] = got

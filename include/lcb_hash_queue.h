@@ -90,6 +90,16 @@ typedef struct lcb_hash_queue_stats_s {
 
 /* Submit flags. */
 #define LCB_HASH_Q_F_NOWAIT	0x0001u	/* EAGAIN instead of waiting for a slot. */
+/* Zero copy: the packet lies in a page-locked region registered with
+ * lcb_hash_queue_register() (e.g. the thread pool's receive io_bufs,
+ * include/utils/io_buf.h:40-47, recvfrom()'d in place,
+ * src/threadpool/threadpool_task.c:692-721): the queue records its address
+ * and length instead of copying its bytes, and the kernel reads it from host
+ * memory over PCIe.  The bytes must stay unchanged until the packet's
+ * completion (digest written / callback called).  One segment only
+ * (lcb_hash_queue_submitv with nsegs == 1); EINVAL if [data, data + size) is
+ * not inside one registered region. */
+#define LCB_HASH_Q_F_ZEROCOPY	0x0002u
 
 /* Defaults: 65536 packets, 16 MiB, 200 us, 4 slots, 16-byte alignment. */
 void	lcb_hash_queue_settings_def(lcb_hash_queue_settings_p s);
@@ -106,6 +116,12 @@ int	lcb_hash_queue_submit(lcb_hash_queue_p q, const uint8_t *data,
 int	lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t *segs,
 	    size_t nsegs, uint8_t *digest, lcb_hash_done_cb cb, void *udata,
 	    uint32_t flags);
+
+/* Register page-locked host memory (hipHostMalloc / hipHostRegister) as a
+ * zero-copy packet source, for the queue's lifetime; up to 16 regions.
+ * EINVAL if [base, base + size) is not page-locked memory of one allocation,
+ * ENOMEM when the table is full.  Call before the submits that use it. */
+int	lcb_hash_queue_register(lcb_hash_queue_p q, const void *base, size_t size);
 
 /* Seal the open batch now (returns at once). */
 int	lcb_hash_queue_flush(lcb_hash_queue_p q);

@@ -108,6 +108,7 @@ class Seg(ctypes.Structure):
 # void cb(void *udata, int error, const uint8_t *digest, size_t digest_size)
 DONE_CB = ctypes.CFUNCTYPE(None, c_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), c_sz)
 Q_F_NOWAIT = 0x1
+Q_F_ZEROCOPY = 0x2
 
 # every symbol include/lcb_hash_queue.h declares
 QUEUE_SIGNATURES = [
@@ -118,6 +119,7 @@ QUEUE_SIGNATURES = [
     ("lcb_hash_queue_submit", ctypes.c_int, [c_vp, c_vp, c_sz, c_vp, DONE_CB, c_vp, c_u32]),
     ("lcb_hash_queue_submitv", ctypes.c_int,
      [c_vp, ctypes.POINTER(Seg), c_sz, c_vp, DONE_CB, c_vp, c_u32]),
+    ("lcb_hash_queue_register", ctypes.c_int, [c_vp, c_vp, c_sz]),
     ("lcb_hash_queue_flush", ctypes.c_int, [c_vp]),
     ("lcb_hash_queue_wait", ctypes.c_int, [c_vp]),
     ("lcb_hash_queue_stats", ctypes.c_int, [c_vp, ctypes.POINTER(QueueStats)]),

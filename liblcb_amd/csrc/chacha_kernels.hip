@@ -20,13 +20,10 @@
 // byte paths.  Waves grid-stride over 64-block tiles, a few tiles each, and
 // every wave's exit condition is the block total it reads.
 //
-// chacha_kernel (compiled out, LCB_CHA_QUAD=1): FOUR LANES PER BLOCK, lane q
-// holding column q; the diagonal round rotates rows 1-3 by DPP quad_perm
-// (folded into the consuming v_add/v_xor by the compiler) and a two-stage
-// DPP transpose gives lane q bytes [16q, 16q+16) for coalesced stores.
-// Measured: same register-only VALU rate as the lane layout, but more
-// per-block overhead (every lane of the quad redoes the block bookkeeping);
-// 0.59-0.67 ms ChaCha20 vs 0.55 for the lane kernel.  Kept for A/B.
+// A four-lanes-per-block formulation (DPP quad rotations, round 1) ran at
+// the same register-only VALU rate with more per-block overhead (0.59-0.67
+// ms ChaCha20 against 0.55); it is gone from the source (git history,
+// profiles/r1_chacha_bench_v*.txt).
 //
 // Block -> buffer: fixed-length batches divide once per wave and then step
 // (bpb blocks per buffer); ragged batches search an exclusive prefix of
@@ -42,25 +39,12 @@
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
 
-#ifndef LCB_CHA_B
-#define LCB_CHA_B 1
-#endif
-#ifndef LCB_CHA_PREFETCH_MAXDR
-#define LCB_CHA_PREFETCH_MAXDR 6
-#endif
 
 namespace lcbgpu {
 
-// DPP quad_perm controls: lane q reads lane p_q of its quad.
-constexpr int kQpRot1 = 0x39;   // [1,2,3,0]  lane q <- q+1
-constexpr int kQpRot2 = 0x4E;   // [2,3,0,1]  lane q <- q+2
-constexpr int kQpRot3 = 0x93;   // [3,0,1,2]  lane q <- q+3
-constexpr int kQpSwp1 = 0xB1;   // [1,0,3,2]  lane q <- q^1
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t qperm(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
-}
+// Double-round counts up to this prefetch the next tile's input while the
+// current one computes (the short ciphers are HBM-bound; ChaCha20 is not).
+constexpr int kChaPrefetchMaxDr = 6;
 
 // chacha.h:125-130
 __device__ __forceinline__ void cha_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
@@ -70,25 +54,12 @@ __device__ __forceinline__ void cha_qr(uint32_t& a, uint32_t& b, uint32_t& c, ui
     c += d; b = rotl32(b ^ c, 7);
 }
 
-// One double round (chacha.h:132-141) of the quad formulation: lane q holds
-// column q as (a, b, c, d) = rows 0..3.
-__device__ __forceinline__ void cha_dround_quad(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
-    cha_qr(a, b, c, d);                                            // columns
-    b = qperm<kQpRot1>(b); c = qperm<kQpRot2>(c); d = qperm<kQpRot3>(d);
-    cha_qr(a, b, c, d);                                            // diagonals
-    b = qperm<kQpRot3>(b); c = qperm<kQpRot2>(c); d = qperm<kQpRot1>(d);
-}
-
 // Whole-state double round in one lane (hchacha prep).
 __device__ __forceinline__ void cha_dround_full(uint32_t* x) {
     cha_qr(x[0], x[4], x[8], x[12]); cha_qr(x[1], x[5], x[9], x[13]);
     cha_qr(x[2], x[6], x[10], x[14]); cha_qr(x[3], x[7], x[11], x[15]);
     cha_qr(x[0], x[5], x[10], x[15]); cha_qr(x[1], x[6], x[11], x[12]);
     cha_qr(x[2], x[7], x[8], x[13]); cha_qr(x[3], x[4], x[9], x[14]);
-}
-
-__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-    return q == 0 ? v0 : (q == 1 ? v1 : (q == 2 ? v2 : v3));
 }
 
 // ----------------------------------------------------------- hchacha prep
@@ -262,144 +233,6 @@ __device__ __forceinline__ void cha_store_slice(uint8_t* d, const uint8_t* s, ui
     }
 }
 
-template <int DR, int B>
-__global__ __launch_bounds__(256) void chacha_kernel(ChaArgs a) {
-    const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, quad = lane >> 2;
-    // Wave-uniform tile bookkeeping (readfirstlane: the compiler cannot see
-    // that threadIdx.x >> 6 is uniform, and would keep it all in VGPRs).
-    const uint64_t wave0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                           (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint64_t total = a.total_blocks;
-    if (a.lengths) {
-        const uint64_t tv = gptr(a.blk_start)[a.count];
-        total = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tv >> 32)) << 32) |
-                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tv);
-    }
-    const uint32_t dr = a.dr;
-    // Column q, rows 0-2 (constants and key), shared by every block unless
-    // the key is per buffer (xchacha subkeys).
-    const uint32_t r0 = sel4(q, a.cst[0], a.cst[1], a.cst[2], a.cst[3]);
-    const uint32_t k1 = sel4(q, a.key[0], a.key[1], a.key[2], a.key[3]);
-    const uint32_t k2 = sel4(q, a.key[4], a.key[5], a.key[6], a.key[7]);
-    // All-ones where this lane keeps its own odd (keep1) / upper-half (keep2)
-    // registers in the two transpose stages.
-    const uint32_t keep1 = (q & 1u) ? 0xffffffffu : 0u, keep2 = (q & 2u) ? 0xffffffffu : 0u;
-    constexpr uint64_t kTile = 16u * B;
-    // Fixed layout: (buf0, jb0) of the tile's first block, advanced by the
-    // grid stride without dividing again.
-    const uint64_t bpb = a.bpb;
-    const uint64_t gstep = nwaves * kTile;
-    uint64_t buf0 = 0, jb0 = 0, sdiv = 0, smod = 0;
-    if (!a.lengths) {
-        buf0 = (wave0 * kTile) / bpb;
-        jb0 = wave0 * kTile - buf0 * bpb;
-        sdiv = gstep / bpb;
-        smod = gstep - sdiv * bpb;
-    }
-    for (uint64_t t = wave0; t * kTile < total; t += nwaves) {
-        const uint64_t g0 = t * kTile;
-        if (a.lengths) buf0 = cha_wave_search(gptr(a.blk_start), a.count, g0, lane);
-        uint32_t x0[B], x1[B], x2[B], x3[B], o1[B], o2[B], o3[B], n[B];
-        uint64_t boff[B];
-#pragma unroll
-        for (int j = 0; j < B; ++j) {
-            const uint32_t d = (uint32_t)j * 16u + quad;
-            uint64_t g = g0 + d;
-            const bool live = g < total;
-            if (!live) g = total - 1;  // compute on a valid block, store nothing
-            uint64_t buf, jb;
-            if (a.lengths) {
-                buf = cha_lane_search(gptr(a.blk_start), a.count, buf0, g);
-                jb = g - gptr(a.blk_start)[buf];
-            } else if (bpb >= kTile) {  // at most one buffer boundary inside the tile
-                jb = jb0 + d;
-                buf = buf0;
-                if (jb >= bpb) {
-                    jb -= bpb;
-                    ++buf;
-                }
-                if (buf >= a.count) buf = a.count - 1;  // dead lane past the end: stores nothing
-            } else {  // short buffers: small 32-bit division
-                const uint32_t r = (uint32_t)jb0 + d;
-                const uint32_t k = r / (uint32_t)bpb;
-                buf = buf0 + k;
-                jb = r - k * (uint32_t)bpb;
-                if (buf >= a.count) buf = a.count - 1;
-            }
-            const uint64_t off = a.offsets ? gptr(a.offsets)[buf] : buf * a.stride;
-            const uint64_t len = a.lengths ? (uint64_t)gptr(a.lengths)[buf] : (uint64_t)a.fixed_len;
-            const uint64_t p = jb * 64u + 16u * q;
-            n[j] = (live && len > p) ? (uint32_t)(len - p < 16u ? len - p : 16u) : 0u;
-            boff[j] = off + p;
-            uint32_t w3;
-            if (q < 2) {  // 64-bit block counter + j (chacha.h:319-327, 440-444)
-                uint64_t ctr = 0;
-                if (a.counters) {
-                    const uint32_t* c = gptr(a.counters) + 2 * buf;
-                    ctr = (uint64_t)c[0] | ((uint64_t)c[1] << 32);
-                }
-                ctr += jb;
-                w3 = q ? (uint32_t)(ctr >> 32) : (uint32_t)ctr;
-            } else {  // IV words (chacha.h:344-355)
-                w3 = a.ivs ? gptr(a.ivs)[buf * a.iv_words + a.iv_at + (q - 2)] : 0u;
-            }
-            uint32_t kk1 = k1, kk2 = k2;
-            if (a.subkeys) {
-                const uint32_t* sk = gptr(a.subkeys) + 8 * buf;
-                kk1 = sk[q];
-                kk2 = sk[4 + q];
-            }
-            x0[j] = r0; x1[j] = o1[j] = kk1; x2[j] = o2[j] = kk2; x3[j] = o3[j] = w3;
-        }
-        // Fully unrolled for the standard round counts so the un-rotation
-        // DPP of one double round folds into the next one's first ops.
-        if (DR) {
-#pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)DR; ++r) {
-#pragma unroll
-                for (int j = 0; j < B; ++j) cha_dround_quad(x0[j], x1[j], x2[j], x3[j]);
-            }
-        } else {
-            for (uint32_t r = 0; r < dr; ++r) {
-#pragma unroll
-                for (int j = 0; j < B; ++j) cha_dround_quad(x0[j], x1[j], x2[j], x3[j]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < B; ++j) {
-            // Feed-forward (chacha.h:143-161): lane q holds words 4r + q.
-            uint32_t m[4] = {x0[j] + r0, x1[j] + o1[j], x2[j] + o2[j], x3[j] + o3[j]};
-            // Transpose the quad's 4x4 so lane q holds words 4q + r.
-            // The selects are bitwise (v_bitop3) on purpose: written as `?:`
-            // the compiler turns them into exec-masked branches and sinks the
-            // DPP read into them, where the partner lane is masked off.
-            uint32_t t1[4], K[4], sw[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sw[r] = qperm<kQpSwp1>(m[r ^ 1]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t1[r] = ch3((r & 1) ? keep1 : ~keep1, m[r], sw[r]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sw[r] = qperm<kQpRot2>(t1[r ^ 2]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) K[r] = ch3((r & 2) ? keep2 : ~keep2, t1[r], sw[r]);
-            if (n[j]) {
-                uint8_t* d = gptr(a.dst) + boff[j];
-                const uint8_t* s = a.src ? gptr(a.src) + boff[j] : nullptr;
-                cha_store_slice(d, s, n[j], K);
-            }
-        }
-        if (!a.lengths) {
-            buf0 += sdiv;
-            jb0 += smod;
-            if (jb0 >= bpb) {
-                jb0 -= bpb;
-                ++buf0;
-            }
-        }
-    }
-}
-
 // ------------------------------------------------- lane-per-block kernel
 // One lane per 64-byte block: the whole 4x4 state in 16 VGPRs, no
 // cross-lane traffic.  Per block this is the minimum VALU work (80 quarter
@@ -476,7 +309,7 @@ __global__ __launch_bounds__(256) void chacha_lane_kernel(ChaArgs a) {
         // Prefetch the source before the rounds when they are short (the
         // memory-bound ChaCha8/12); for long rounds load after them and keep
         // the 16 VGPRs for occupancy instead.
-        constexpr bool kPrefetch = DR != 0 && DR <= LCB_CHA_PREFETCH_MAXDR;
+        constexpr bool kPrefetch = DR != 0 && DR <= kChaPrefetchMaxDr;
         uint4 in[4] = {};
         if (kPrefetch && stream && a.src) {
             const uint4* sb = reinterpret_cast<const uint4*>(gptr(a.src) + g0 * 64u);
@@ -582,9 +415,6 @@ __global__ __launch_bounds__(256) void chacha_lane_kernel(ChaArgs a) {
     }
 }
 
-#ifndef LCB_CHA_QUAD
-#define LCB_CHA_QUAD 0
-#endif
 
 // Workgroups that are resident at once on the whole device for kernel K
 // (CUs x occupancy), cached per device: the persistent grid is sized to it so
@@ -611,19 +441,13 @@ static uint64_t resident_grid(K kernel) {
 // API (which can over-count residency by one workgroup per CU at some SGPR
 // counts, MI355X_MICROARCH.md 'Residency').  Ragged batches (total unknown on
 // the host) launch 8x the resident count and grid-stride.
-#ifndef LCB_CHA_TILES_PER_WAVE
-#define LCB_CHA_TILES_PER_WAVE 4
-#endif
+constexpr uint64_t kChaTilesPerWave = 4;
 template <int DR>
 static void launch_cha_dr(const ChaArgs& a, uint64_t need_tiles, hipStream_t s) {
-#if LCB_CHA_QUAD
-    auto kern = chacha_kernel<DR, LCB_CHA_B>;
-#else
     auto kern = chacha_lane_kernel<DR>;
-#endif
     uint64_t grid = need_tiles == UINT64_MAX
                         ? 8 * resident_grid(kern)
-                        : (need_tiles + 4 * LCB_CHA_TILES_PER_WAVE - 1) / (4 * LCB_CHA_TILES_PER_WAVE);
+                        : (need_tiles + 4 * kChaTilesPerWave - 1) / (4 * kChaTilesPerWave);
     grid = std::min<uint64_t>(std::max<uint64_t>(grid, 1), 1u << 20);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, s, a);
 }
@@ -645,7 +469,7 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
         k.subkeys = subkeys;
     }
     // Grid sizing: see launch_cha_dr.
-    constexpr uint64_t kTile = LCB_CHA_QUAD ? 16u * LCB_CHA_B : 64u;
+    constexpr uint64_t kTile = 64u;
     uint64_t need = UINT64_MAX;  // tiles
     if (!a.lengths) need = (a.total_blocks + kTile - 1) / kTile;
     switch (a.dr) {

@@ -263,9 +263,15 @@ __device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
 #ifndef LCB_GOST_G_ROLLED
 #define LCB_GOST_G_ROLLED 1
 #endif
+using lds_u64w = __attribute__((address_space(3))) uint64_t;
+// ff (optional): LDS slots (stride ff_stride) that hold the feed-forward
+// h ^ m through the 25 LPS instead of 16 VGPRs (the final g_0(h, Sigma),
+// whose Sigma slots are free by then).  Read back volatile, so the compiler
+// does not keep the stored words in registers anyway.
 #if LCB_GOST_G_ROLLED
 template <class Tab>
-__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
+__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T,
+                                       lds_u64w* ff = nullptr, int ff_stride = 0) {
     // E(K, m) as 12 (K, t) steps plus the last key, from K_0 = h, t_0 = m:
     //   step r: K_{r+1} = LPS(K_r ^ c_r), t_{r+1} = LPS(t_r ^ K_{r+1}),
     //   c_0 = N, c_r = C_{r-1};  K_13 = LPS(K_12 ^ C_11) (step 12, no t).
@@ -277,6 +283,7 @@ __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_
         k[i] = h[i];
         t[i] = m[i];
         h[i] ^= m[i];   // the feed-forward h ^ m of :1142, taken now: m and the old h die here
+        if (ff) ff[i * ff_stride] = h[i];
     }
 #pragma unroll 1
     for (int r = 0; r < 13; ++r) {
@@ -294,14 +301,18 @@ __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_
         T.lps(t, x);                                     // t_{r+1} = LPS(t_r ^ K_{r+1})
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] ^= t[i] ^ k[i];     // :1142 (h already holds h ^ m)
+    for (int i = 0; i < 8; ++i) {
+        if (ff) h[i] = *(volatile lds_u64w*)&ff[i * ff_stride];
+        h[i] ^= t[i] ^ k[i];                             // :1142 (h already holds h ^ m)
+    }
 }
 
 #else
 // Unrolled head and tail (round 2's form): K_1, t_1 and K_13 outside the
 // 11-round loop.
 template <class Tab>
-__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T) {
+__device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_t m[8], const Tab& T,
+                                       lds_u64w* = nullptr, int = 0) {
     uint64_t k[8], t[8], x[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = h[i];
@@ -336,7 +347,6 @@ __device__ __forceinline__ void gost_g(uint64_t h[8], uint64_t n0, const uint64_
 // thread x at sgl_base[(i - (8 - kSgLds)) * kSgStride + x] (bind_sigma), not
 // in VGPRs.  Sigma is touched once per block, and its 16 VGPRs are what
 // pushed the batch kernels (4 waves per SIMD, 128 VGPRs) into scratch spills.
-using lds_u64w = __attribute__((address_space(3))) uint64_t;
 template <bool k256, int kSgStride = 0, int kSgLds = 0>
 struct Gost {
     static constexpr int kBlock = 64, kDigest = k256 ? 32 : 64, kWords = 16;
@@ -419,7 +429,8 @@ struct Gost {
 #pragma unroll
         for (int i = 0; i < 8; ++i) m[i] = sigma_final(i);
         T.to_lane(ml, m);
-        gost_g(h, 0, ml, T);   // g_0(h, Sigma)
+        if constexpr (kSgLds == 8) gost_g(h, 0, ml, T, sgl, kSgStride);   // g_0(h, Sigma), h ^ Sigma in the Sigma slots
+        else gost_g(h, 0, ml, T);   // g_0(h, Sigma)
     }
     template <class Tab>
     __device__ __forceinline__ void digest_words(uint32_t* out, const Tab& T) const {

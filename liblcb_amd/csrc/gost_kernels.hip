@@ -30,6 +30,15 @@ __device__ __forceinline__ uint64_t store_index(const KArgs& a, uint64_t base) {
     return a.order ? (uint64_t)gptr(a.order)[i] : i;
 }
 
+// The digest words made final here (empty asm): else the compiler sinks
+// the last LPS's XORs past store_index's branch and keeps its 8-byte table
+// words live across it, which spilled GOST-256 (28 B per lane).
+template <int N>
+__device__ __forceinline__ void settle_words(uint32_t (&w)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(w[i]));
+}
+
 // ------------------------------------------------------------------ GOST
 // One 1024-thread workgroup per CU (16 waves: four per SIMD, so at most 128
 // VGPRs per lane) sharing ONE 64 KiB rotated LPS image (gost_device.hpp
@@ -79,6 +88,7 @@ __global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
         gost_run(st, GostPlainSrc{msg, len}, T);
     }
     st.digest_words(dw, T);
+    settle_words<G::kDigest / 4>(dw);
     store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
     }
 }
@@ -121,6 +131,7 @@ __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
         gost_run(st, GostVirtSrc{msg, len, K, kl}, T);
     }
     st.digest_words(dw, T);
+    settle_words<G::kDigest / 4>(dw);
     store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
     }
 }

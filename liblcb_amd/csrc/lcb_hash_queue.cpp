@@ -59,6 +59,9 @@ constexpr uint32_t kLeaseMsgs = 32;              // message indices per lease
 constexpr size_t kLeaseBytes = 32u << 10;        // arena bytes per lease, at least
 
 inline uint64_t st_count(uint64_t s) { return (s >> kCountShift) & kCountMask; }
+// h_off entry of a zero-copy packet: this bit | its device address (user
+// addresses are far below 2^63); arena packets hold their arena position.
+constexpr uint64_t kZeroCopyTag = 1ull << 63;
 inline uint64_t st_bytes(uint64_t s) { return s & kBytesMask; }
 
 struct Meta {
@@ -185,6 +188,17 @@ struct lcb_hash_queue_s {
     std::atomic<uint64_t> max_fill{0}, max_launch{0}, max_gpu{0}, max_cb{0}, max_submit_wait{0};
     std::atomic<int> first_error{0};
 
+    // Zero-copy packet sources (lcb_hash_queue_register): append-only, read
+    // lock-free by submitters once `nregions` covers an entry.
+    struct Region {
+        const uint8_t* host;
+        size_t size;
+        uint64_t dev;   // device address of host[0]
+    };
+    static constexpr int kMaxRegions = 16;
+    Region regions[kMaxRegions];
+    std::atomic<int> nregions{0};
+
     std::thread flusher, completer;
 
     void flusher_main();
@@ -250,15 +264,21 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
     b->n = st_count(s);
     b->bytes = st_bytes(s);
     size_t payload = 0, packets = 0;
+    // Offsets become absolute device addresses (the batch's `data` is 0):
+    // arena packets at d_data + pos, zero-copy packets where they lie in
+    // host memory (kZeroCopyTag | device address, from the submit).
+    const uint64_t arena = (uint64_t)reinterpret_cast<uintptr_t>(b->d_data);
     for (size_t i = 0; i < b->n; ++i) {
         payload += b->h_len[i];
         packets += b->meta[i].real;
+        const uint64_t o = b->h_off[i];
+        b->h_off[i] = (o & kZeroCopyTag) ? (o & ~kZeroCopyTag) : arena + o;
     }
     b->payload = payload;
     b->packets = packets;
     hipStream_t st = b->stream;
     KArgs a;
-    a.data = b->d_data; a.offsets = b->d_off; a.lengths = b->d_len; a.order = nullptr;
+    a.data = nullptr; a.offsets = b->d_off; a.lengths = b->d_len; a.order = nullptr;
     a.count = b->n; a.stride = 0; a.fixed_len = 0; a.digests = b->d_dig; a.mid = mid;
     int rc = 0;
     if (hipMemcpyAsync(b->d_off, b->h_off, b->n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -318,7 +338,10 @@ void lcb_hash_queue_s::flusher_main() {
         }
         seal(b);  // no-op when a producer already sealed it as full
         b->t_seal = now_ns();
-        note_max(max_fill, b->t_seal - b->t_first.load(std::memory_order_relaxed));
+        // A slot can be sealed full while a lease holder has not published its
+        // first packet yet (t_first still 0): no fill time to report then.
+        const int64_t t_first = b->t_first.load(std::memory_order_relaxed);
+        if (t_first != 0) note_max(max_fill, b->t_seal - t_first);
         flush_req.store(false, std::memory_order_release);
         // Reopen at once when a slot is free (producers then wait only for the
         // install, never for the launch below).  When every other slot is still
@@ -560,13 +583,28 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
 
 int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_t nsegs, uint8_t* digest,
                            lcb_hash_done_cb cb, void* udata, uint32_t flags) {
-    if (!q || (nsegs && !segs) || (flags & ~LCB_HASH_Q_F_NOWAIT)) return EINVAL;
+    if (!q || (nsegs && !segs) || (flags & ~(LCB_HASH_Q_F_NOWAIT | LCB_HASH_Q_F_ZEROCOPY))) return EINVAL;
     size_t len = 0;
     for (size_t k = 0; k < nsegs; ++k) {
         if (segs[k].size && !segs[k].data) return EINVAL;
         len += segs[k].size;
     }
     if (len > UINT32_MAX || len > q->cfg.max_batch_bytes) return EMSGSIZE;
+    // Zero copy: the packet's device address in a registered region; it
+    // takes a batch index but no staging bytes.
+    uint64_t zc = 0;
+    if (flags & LCB_HASH_Q_F_ZEROCOPY) {
+        if (nsegs != 1) return EINVAL;
+        const uint8_t* p = segs[0].data;
+        const int nr = q->nregions.load(std::memory_order_acquire);
+        for (int r = 0; r < nr && !zc; ++r) {
+            const auto& R = q->regions[r];
+            if (p >= R.host && (size_t)(p - R.host) <= R.size && len <= R.size - (size_t)(p - R.host))
+                zc = kZeroCopyTag | (R.dev + (uint64_t)(p - R.host));
+        }
+        if (!zc) return EINVAL;
+    }
+    const size_t clen = zc ? 0 : len;   // staging bytes the packet takes
     const uint64_t A = q->cfg.align;
     const uint64_t cap_m = q->cfg.max_batch_msgs, cap_b = q->cfg.max_batch_bytes, LM = q->lease_msgs;
     Lease& L = tls_lease(q->qid);
@@ -580,20 +618,22 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
             std::atomic_thread_fence(std::memory_order_seq_cst);
             const bool live = b->gen.load(std::memory_order_relaxed) == L.gen &&
                               !b->closed.load(std::memory_order_relaxed);
-            const uint64_t pos = (L.pos + A - 1) & ~(A - 1);
-            if (live && L.idx < L.idx_end && pos + len <= L.pos_end) {
-                uint8_t* dst = b->h_data + pos;
-                for (size_t k = 0; k < nsegs; ++k) {
-                    if (segs[k].size) stream_copy(dst, segs[k].data, segs[k].size);
-                    dst += segs[k].size;
+            const uint64_t pos = zc ? L.pos : (L.pos + A - 1) & ~(A - 1);
+            if (live && L.idx < L.idx_end && pos + clen <= L.pos_end) {
+                if (!zc) {
+                    uint8_t* dst = b->h_data + pos;
+                    for (size_t k = 0; k < nsegs; ++k) {
+                        if (segs[k].size) stream_copy(dst, segs[k].data, segs[k].size);
+                        dst += segs[k].size;
+                    }
+                    _mm_sfence();  // streaming stores before the release of `done`
                 }
-                _mm_sfence();  // streaming stores before the release of `done`
                 const uint64_t i = L.idx;
-                b->h_off[i] = pos;
+                b->h_off[i] = zc ? zc : pos;
                 b->h_len[i] = (uint32_t)len;
                 b->meta[i] = Meta{digest, cb, udata, 1};
                 L.idx = i + 1;
-                L.pos = pos + len;
+                L.pos = pos + clen;
                 r.done.store((uint32_t)(L.idx - (uint64_t)L.rec * LM), std::memory_order_release);
                 r.busy.fetch_sub(1, std::memory_order_release);
                 if (b->t_first.load(std::memory_order_relaxed) == 0) {
@@ -619,7 +659,7 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
             cnt = st_count(s);
             pos0 = (st_bytes(s) + A - 1) & ~(A - 1);
             const uint64_t room = cap_b > pos0 ? cap_b - pos0 : 0;
-            if (cnt + LM > cap_m || room < len) {  // an empty slot always fits
+            if (cnt + LM > cap_m || room < clen) {  // an empty slot always fits
                 if (seal(b)) {
                     { std::lock_guard<std::mutex> lk(q->m); }
                     q->cv_flusher.notify_one();
@@ -627,8 +667,8 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
                 break;
             }
             const uint64_t want = std::max<uint64_t>(q->lease_bytes,
-                                                     std::min<uint64_t>(LM * (len + A), cap_b / 8));
-            nbytes = std::min<uint64_t>(std::max<uint64_t>(want, len), room);
+                                                     std::min<uint64_t>(LM * (clen + A), cap_b / 8));
+            nbytes = std::min<uint64_t>(std::max<uint64_t>(want, clen), room);
             const uint64_t ns = ((cnt + LM) << kCountShift) | (pos0 + nbytes);
             if (b->state.compare_exchange_weak(s, ns, std::memory_order_acq_rel)) {
                 got = true;
@@ -671,6 +711,29 @@ int lcb_hash_queue_submit(lcb_hash_queue_p q, const uint8_t* data, size_t size, 
     if (size && !data) return EINVAL;
     lcb_hash_seg_t seg{data, size};
     return lcb_hash_queue_submitv(q, &seg, 1, digest, cb, udata, flags);
+}
+
+int lcb_hash_queue_register(lcb_hash_queue_p q, const void* base, size_t size) {
+    if (!q || !base || size == 0) return EINVAL;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, base) != hipSuccess) {
+        (void)hipGetLastError();
+        return EINVAL;   // pageable memory
+    }
+    if (attr.type != hipMemoryTypeHost || !attr.devicePointer) return EINVAL;
+    const void* last = static_cast<const uint8_t*>(base) + size - 1;
+    hipPointerAttribute_t al;
+    if (hipPointerGetAttributes(&al, last) != hipSuccess || al.type != hipMemoryTypeHost ||
+        static_cast<const uint8_t*>(al.devicePointer) != static_cast<const uint8_t*>(attr.devicePointer) + size - 1) {
+        (void)hipGetLastError();
+        return EINVAL;   // not one page-locked allocation
+    }
+    std::lock_guard<std::mutex> lk(q->m);
+    const int n = q->nregions.load(std::memory_order_relaxed);
+    if (n >= lcb_hash_queue_s::kMaxRegions) return ENOMEM;
+    q->regions[n] = {static_cast<const uint8_t*>(base), size, (uint64_t)reinterpret_cast<uintptr_t>(attr.devicePointer)};
+    q->nregions.store(n + 1, std::memory_order_release);
+    return 0;
 }
 
 int lcb_hash_queue_flush(lcb_hash_queue_p q) {

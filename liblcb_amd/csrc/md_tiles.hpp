@@ -57,6 +57,12 @@ enum { kTilePlain = 0, kTileHmac = 1, kTileKeyedHmac = 2, kTileKeyedSuffix = 3 }
 constexpr int kTileWaves = 4;     // waves per workgroup (one 8 KiB slab each)
 constexpr int kTileWgPerCu = 4;   // 4 waves per SIMD (kTileOcc): 128 KiB of LDS
 
+// __builtin_amdgcn_readfirstlane is 32-bit: a 64-bit value goes as two halves.
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
     return k < a.nkeys ? k : a.nkeys - 1;   // never out of range: lcb_hash_batch_keyed checked the indices
@@ -161,8 +167,7 @@ __device__ __forceinline__ void tile_compress(H& st, const uint32_t* w) {
 
 // Block b of a lane's (virtual) message from the streamed words w: whole
 // message blocks go straight to compress; the block holding the message's
-// end gets its bytes past the end cleared, the suffix key's bytes (keyed
-// suffix), the 0x80 terminator and, in the last block, the bit length of
+// end gets its bytes past the end cleared, the 0x80 terminator and, in the last block, the bit length of
 // prefix + total (md5.h:266-288).  Lanes whose message has fewer blocks do
 // nothing.  nfull_min: wave minimum of whole message blocks (uniform fast path).
 template <class H, int kMode>
@@ -181,15 +186,24 @@ __device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint6
             const int v = rb - 4 * k;
             w[k] &= v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu >> (32 - 8 * v)));
         }
-        if (kMode == kTileKeyedSuffix) {
-            const uint64_t e = pos + 64 < m.total ? pos + 64 : m.total;   // key bytes [max(pos, len), e)
-            const uint64_t s0 = pos > len ? pos : len;
-            if (s0 < e) or_window64(m.K + pos - len, (uint32_t)(s0 - pos), (uint32_t)(e - pos), w);
-        }
         if (m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
         if (b + 1 == nblk) H::put_length(w, m.total + m.prefix);
     }
     tile_compress(st, w);
+}
+
+// Initial state, materialised inside the tile loop: as plain constants the
+// compiler hoists them out of the persistent loop and spills them.
+template <class H>
+__device__ __forceinline__ void tile_init(H& st) {
+    if constexpr (std::is_same<H, Md5>::value) {
+        asm volatile("v_mov_b32 %0, 0x67452301" : "=v"(st.s[0]));
+        asm volatile("v_mov_b32 %0, 0xefcdab89" : "=v"(st.s[1]));
+        asm volatile("v_mov_b32 %0, 0x98badcfe" : "=v"(st.s[2]));
+        asm volatile("v_mov_b32 %0, 0x10325476" : "=v"(st.s[3]));
+    } else {
+        st.init();
+    }
 }
 
 template <class H, int kMode>
@@ -219,7 +233,7 @@ __device__ __forceinline__ void tile_state(const KArgs& a, const TileRec& r, H& 
         load_words(st.s, mid);              // state after K ^ ipad
         m.prefix = H::kBlock;
     } else {
-        st.init();
+        tile_init(st);
     }
     if (kMode == kTileKeyedSuffix) {
         const uint32_t k = key_of(a, r.idx);
@@ -240,47 +254,85 @@ __device__ __forceinline__ void md_tile_direct(const KArgs& a, const TileRec& r)
     tile_finish<H, kMode>(a, st, r);
 }
 
-// The tile's line stream: lane l owns record l.  Line L of the 64 records
-// moves into the wave's 8 KiB slab with 8 global_load_lds_dwordx4, instruction
-// g carrying chunk g (bytes 16 g .. 16 g + 15) of every record's line, so
-// slot (g, l) = slab + 1024 g + 16 l, and lane l reads its line back with 8
-// conflict-free ds_read_b128 (16 consecutive lanes read 256 contiguous bytes).
-// Per lane: one 64-bit line address (2 VGPRs; the 8 chunk addresses are
-// formed at issue), against 8 per-lane record pointers (16 VGPRs) in the
-// fixed kernel's 8-records-per-instruction layout.  A chunk that holds no
-// byte of the lane's record (the last lines of a tile) is fetched from the
-// record's first chunk instead: same page, never used.
-struct LaneLineStream {
+// The tile's line stream: line L of the 64 records moves into the wave's
+// 8 KiB slab with 8 global_load_lds_dwordx4.  Lane group q (lanes 8q ..
+// 8q + 7) carries, in instruction g, the whole 128-B line of record 8q + g
+// (one of its own lanes' records), lane 8q + c its chunk c ^ g: the texture
+// unit sees 8 whole lines per instruction, not 64 partial ones, and what a
+// DMA lane needs of the record it moves comes from inside its 8-lane group.
+// Instruction g lands at slab row 8g + q, so record j's line is row
+// R(j) = 8 (j & 7) + (j >> 3), its chunk k in slot k ^ (j & 7): the 16 lanes
+// of a ds_read_b128 group hit 16 different bank groups.
+// Addressing: the saddr form, a wave-uniform scalar base (the tile's lowest
+// stream base + 128 L) plus one 32-bit offset per instruction (8 VGPRs;
+// md_tile_stream checks that the tile spans less than 4 GiB).  In the last
+// lines (masked) a chunk that holds no byte of its record is fetched from
+// the record's first chunk instead: same page, the data never used.  Which
+// chunks are valid comes from one word per group per line: every lane's
+// count of valid chunks in the line, 4 bits each, OR-reduced in the group.
+struct TileGatherStream {
     uint8_t* slab;
-    const uint8_t* line;   // this lane's record, current line
-    __device__ __forceinline__ void init(const uint8_t* base, uint8_t* my_slab) {
+    uint32_t lane;
+    const uint8_t* tb;      // wave-uniform: the tile's lowest stream base
+    uint32_t voff[8];       // instruction g: this lane's chunk of record 8 (lane >> 3) + g, bytes from tb
+    __device__ __forceinline__ void init(const uint8_t* tile_base, uint32_t rel, uint32_t ln, uint8_t* my_slab) {
+        lane = ln;
         slab = my_slab;
-        line = base;
-    }
-    template <int kAux>
-    __device__ __forceinline__ void issue(uint32_t L, bool masked, uint64_t end, const uint8_t* base) {
+        tb = tile_base;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint8_t* src = line + 16 * g;
-            if (masked) src = (uint64_t)L * 128u + 16u * g < end ? src : base;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+            const uint32_t rj = (uint32_t)__shfl((int)rel, (int)(ln & ~7u) + g, 64);
+            voff[g] = rj + ((ln & 7u) ^ (uint32_t)g) * 16u;
+        }
+    }
+    template <int kAux>
+    __device__ __forceinline__ void issue(uint32_t L) {
+        asm volatile("" : "+v"(voff[0]), "+v"(voff[1]), "+v"(voff[2]), "+v"(voff[3]), "+v"(voff[4]),
+                     "+v"(voff[5]), "+v"(voff[6]), "+v"(voff[7]));
+        uint64_t so = (uint64_t)L * 128u;
+        asm volatile("" : "+s"(so));
+        const uint8_t* sb = tb + so;
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g]),
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
+    }
+    // lastc: index of this lane's last stream chunk holding a record byte.
+    template <int kAux>
+    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc) {
+        // The lane id re-defined per call: the per-lane chunk numbers below
+        // are not hoisted out of the tile loop (16 VGPRs held all along).
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        int n = (int)lastc - 8 * (int)L + 1;                    // valid chunks of line L
+        n = n < 0 ? 0 : (n > 8 ? 8 : n);
+        uint32_t nv = (uint32_t)n << (4u * (ln & 7u));
+        nv |= (uint32_t)__shfl_xor((int)nv, 1, 64);
+        nv |= (uint32_t)__shfl_xor((int)nv, 2, 64);
+        nv |= (uint32_t)__shfl_xor((int)nv, 4, 64);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t k = (ln & 7u) ^ (uint32_t)g;
+            const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
         }
-        line += 128;
     }
-    // Waits for the issued line and copies this lane's 128 B (raw LE words).
-    __device__ __forceinline__ void take(uint32_t y[32], uint32_t lane) const {
+    // Waits for the issued line, copies this lane's 128 B (raw LE words); the
+    // slab is free again on return.
+    __device__ __forceinline__ void take(uint32_t y[32]) const {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         using lds_cu4 = __attribute__((address_space(3))) const v4u;
-        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) + lane * 16;
+        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) +
+                     (8u * (lane & 7u) + (lane >> 3)) * 128u + (lane & 7u) * 16u;
         asm volatile("" : "+v"(b));
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const v4u v = *(lds_cu4*)(uintptr_t)(b + (uint32_t)(g * 1024));
-            y[4 * g] = v.x; y[4 * g + 1] = v.y; y[4 * g + 2] = v.z; y[4 * g + 3] = v.w;
+        for (int k = 0; k < 8; ++k) {
+            const v4u v = *(lds_cu4*)(uintptr_t)(b ^ (uint32_t)(k << 4));
+            y[4 * k] = v.x; y[4 * k + 1] = v.y; y[4 * k + 2] = v.z; y[4 * k + 3] = v.w;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab free again
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 };
 
@@ -312,13 +364,34 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     NB = __builtin_amdgcn_readfirstlane(NB);
     NS = __builtin_amdgcn_readfirstlane(NS);
     NF = __builtin_amdgcn_readfirstlane(NF);
-    const uint8_t* base = r.p - off0;
-    LaneLineStream ls;
-    ls.init(base, slab);
+    // The tile's stream bases: 32-bit offsets from the lowest (saddr form)
+    // when the tile spans less than 4 GiB, else the per-lane loop.
+    const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off0;
+    uint64_t lo = base, hi = base;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d, 64));
+        hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d, 64));
+    }
+    lo = readfirstlane64(lo);
+    hi = readfirstlane64(hi);
+    if (hi - lo + (uint64_t)(NL + 1) * 128u >= (1ull << 32) || !__all(end != 0)) {
+        if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m.K, m.kl, 0);
+        else md_message(st, r.p, r.len, m.prefix);
+        tile_finish<H, kMode>(a, st, r);
+        return;
+    }
+    const uint32_t lastc = (uint32_t)((end - 1) >> 4);
+    TileGatherStream ls;
+    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(base - lo), lane, slab);
     auto issue = [&](uint32_t L) {
-        const bool masked = L >= NS;
-        if (whole_lines) ls.issue<kLdsAux>(L, masked, end, base);
-        else ls.issue<kGatherAux>(L, masked, end, base);
+        if (L >= NS) {
+            if (whole_lines) ls.issue_masked<kLdsAux>(L, lastc);
+            else ls.issue_masked<kGatherAux>(L, lastc);
+        } else {
+            if (whole_lines) ls.issue<kLdsAux>(L);
+            else ls.issue<kGatherAux>(L);
+        }
     };
     const uint32_t c0 = NL > 3 ? NL - 3 : 0u;                // first claim step
     if (NL) issue(0);
@@ -326,11 +399,16 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // Whole-block lines: both blocks of line L (2L - 1 and 2L) are whole
     // message blocks of every lane (2L < NF).
     const uint32_t LF = (NF + 1) / 2 < NL ? (NF + 1) / 2 : NL;
+    // Keyed suffix: the stream ends with the whole-block lines, the rest
+    // (under two lines of message, the key) goes through the per-lane loop:
+    // the key's window assembly next to a streamed line needs more VGPRs
+    // than the occupancy leaves.
+    const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
     uint32_t L = 0;
     for (; L < LF; ++L) {
         uint32_t y[32];
-        ls.take(y, lane);
-        if (L + 1 < NL) issue(L + 1);
+        ls.take(y);
+        if (L + 1 < LE) issue(L + 1);
         if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         uint32_t w[16];
         if (L > 0) {   // block 2L - 1: the carry and dwords 0..Q of this line
@@ -342,38 +420,37 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
     }
-    // The rest, one block per step (tile_block: ends of messages, padding,
-    // length, suffix key bytes).  Block b = 2L - 1 takes line L (zeros past
-    // the last line: those bytes lie past every record's end) and assembles
-    // block 2L from it at once, kept in `wn` (16 VGPRs, not the whole line)
-    // for the next step.
-    uint32_t wn[16];
-    for (uint32_t b = LF ? 2 * LF - 1 : 0; b < NB; ++b) {
-        uint32_t w[16];
-        if ((b & 1) || b == 0) {        // wave-uniform
-            uint32_t y[32];
-            L = (b + 1) >> 1;
-            if (L < NL) {
-                ls.take(y, lane);
-                if (L + 1 < NL) issue(L + 1);
-                if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 32; ++k) y[k] = 0u;
-            }
-            if (b & 1) {
-                tile_assemble(Q, c, y, sh, w);
-                tile_assemble(Q, y, y + 16, sh, wn);
-            } else {                    // b == 0
-                tile_assemble(Q, y, y + 16, sh, w);
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+    if constexpr (kMode == kTileKeyedSuffix) {
+        const uint64_t done = LF ? (2ull * LF - 1) * 64u : 0u;   // blocks 0 .. 2 LF - 2
+        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
+        md_message2(st, r.p + done, len - done, m.K, m.kl, m.prefix + done);
+        tile_finish<H, kMode>(a, st, r);
+        return;
+    }
+    // The rest, line by line (tile_block: ends of messages, padding, length);
+    // lines past the last streamed one are zeros (those bytes lie past every
+    // record's end).
+    for (; 2 * L <= NB; ++L) {   // block 2L - 1 < NB
+        uint32_t y[32];
+        if (L < NL) {
+            ls.take(y);
+            if (L + 1 < NL) issue(L + 1);
+            if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = wn[k];
+            for (int k = 0; k < 32; ++k) y[k] = 0u;
         }
-        tile_block<H, kMode>(st, b, w, len, m, nblk, NF);
+        uint32_t w[16];
+        if (L > 0) {
+            tile_assemble(Q, c, y, sh, w);
+            tile_block<H, kMode>(st, 2 * L - 1, w, len, m, nblk, NF);
+        }
+        if (2 * L < NB) {
+            tile_assemble(Q, y, y + 16, sh, w);
+            tile_block<H, kMode>(st, 2 * L, w, len, m, nblk, NF);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
     }
     tile_finish<H, kMode>(a, st, r);
 }
@@ -391,6 +468,11 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
     while (cl.t < ntiles) {
         const TileRec r = cl.r;
         cl.stage = 0;
+        // The lane id re-defined per tile: what the tile derives from it
+        // (bpermute addresses, slab slots, chunk numbers) is formed per tile
+        // instead of being hoisted out of the loop into VGPRs held all along.
+        uint32_t lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
         // The tile's phase: Q (uniform) or a mixed tile.
         // Q: 16 for a record on the second half of a 128-B line, 0 on its
         // first half (both: the stream is whole cache lines), else the

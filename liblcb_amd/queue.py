@@ -6,6 +6,9 @@ HashQueue is the batching replacement: `submit` copies the packet into the
 open page-locked batch and returns; the digest arrives later in `out` and/or
 through `cb(error, digest_bytes)`, called on the library's completion thread
 (the tpt_msg_send() delivery point, src/threadpool/threadpool_msg_sys.c:279).
+Zero copy: `register` a page-locked receive area (e.g. a pinned torch tensor's
+numpy view) and `submit(..., zerocopy=True)` packets lying in it -- the queue
+records where they are and the kernel reads them in place.
 
 All hashing happens in the HIP kernels of liblcb_hash_gpu.so; there is no
 CPU path.
@@ -16,8 +19,8 @@ import threading
 
 import numpy as np
 
-from ._lib import (DIGEST_SIZE, DONE_CB, Q_F_NOWAIT, QueueSettings, QueueStats, Seg, c_vp, check,
-                   lib)
+from ._lib import (DIGEST_SIZE, DONE_CB, Q_F_NOWAIT, Q_F_ZEROCOPY, QueueSettings, QueueStats, Seg, c_vp,
+                   check, lib)
 
 __all__ = ["HashQueue"]
 
@@ -53,7 +56,8 @@ class HashQueue:
         self._lock = threading.Lock()
         self._ids = itertools.count(1)
         self._cbs = {}          # udata id -> python callable
-        self._outs = []         # digest arrays kept alive until wait()
+        self._outs = []         # digest arrays (and zero-copy packets) kept alive until wait()
+        self._regions = []      # registered page-locked areas
         self._trampoline = DONE_CB(self._on_done)
 
     def _on_done(self, udata, error, digest, size):
@@ -62,7 +66,22 @@ class HashQueue:
         if fn is not None:
             fn(error, bytes(digest[:size]) if error == 0 else None)
 
-    def _submit(self, segs, out, cb, nowait):
+    def register(self, area):
+        """Register a page-locked uint8 area (numpy view of pinned memory, or
+        a pinned CPU torch tensor) as a zero-copy packet source."""
+        if hasattr(area, "data_ptr"):
+            if not area.is_pinned():
+                raise ValueError("torch tensor must be pinned")
+            p, n = area.data_ptr(), area.numel() * area.element_size()
+        else:
+            a = np.asarray(area)
+            if not a.flags.c_contiguous:
+                raise ValueError("area must be contiguous")
+            p, n = a.ctypes.data, a.nbytes
+        check(lib().lcb_hash_queue_register(self._q, p, n))
+        self._regions.append(area)
+
+    def _submit(self, segs, out, cb, nowait, zerocopy=False):
         L = lib()
         op = None
         if out is not None:
@@ -77,25 +96,32 @@ class HashQueue:
         arr = (Seg * max(1, len(segs)))()
         keep = []
         for i, x in enumerate(segs):
+            if zerocopy and not (isinstance(x, np.ndarray) and x.flags.c_contiguous):
+                raise ValueError("a zero-copy packet is a contiguous numpy view of a registered area")
             p, n, k = _buf(x)
             arr[i].data, arr[i].size = p, n
             keep.append(k)
+        flags = (Q_F_NOWAIT if nowait else 0) | (Q_F_ZEROCOPY if zerocopy else 0)
         rc = L.lcb_hash_queue_submitv(self._q, arr, len(segs), op,
                                       self._trampoline if cb is not None else DONE_CB(),
-                                      uid or None, Q_F_NOWAIT if nowait else 0)
+                                      uid or None, flags)
         if rc != 0 and uid:
             with self._lock:
                 self._cbs.pop(uid, None)
         check(rc)
-        if out is not None:
+        if out is not None or zerocopy:
             with self._lock:
-                self._outs.append(out)
+                if out is not None:
+                    self._outs.append(out)
+                if zerocopy:
+                    self._outs.append(keep)
 
-    def submit(self, data, out=None, cb=None, nowait=False):
+    def submit(self, data, out=None, cb=None, nowait=False, zerocopy=False):
         """Queue one packet.  `out` (uint8[D]) receives the digest; `cb(error,
         digest)` is called on the completion thread.  Both stay pending until
-        completion (see wait())."""
-        self._submit([data], out, cb, nowait)
+        completion (see wait()).  zerocopy: `data` lies in a registered area
+        and must stay unchanged until completion (LCB_HASH_Q_F_ZEROCOPY)."""
+        self._submit([data], out, cb, nowait, zerocopy)
 
     def submitv(self, segs, out=None, cb=None, nowait=False):
         """Queue one packet given as segments (hashed as their concatenation)."""
@@ -121,6 +147,7 @@ class HashQueue:
             lib().lcb_hash_queue_destroy(self._q)
             self._q = None
             self._outs.clear()
+            self._regions.clear()
 
     def __enter__(self):
         return self

@@ -287,3 +287,101 @@ def test_stale_lease_across_generations(gpu, oracle):
         st = q.stats()
     assert np.array_equal(got, want)
     assert st["packets"] == len(pkts) and st["batches"] > 50
+
+
+# ------------------------------------------------------------ zero copy
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,key", [(MD5, None), (MD5, b"radius-shared-secret"), (SHA256, None)])
+def test_zerocopy_submit(gpu, oracle, alg, key):
+    """LCB_HASH_Q_F_ZEROCOPY: packets at byte offsets inside a registered
+    pinned area, hashed in place (mixed with copied submits), from several
+    threads, over many batches; digests == oracle."""
+    import torch
+    from liblcb_amd.queue import HashQueue
+    from liblcb_amd._lib import DIGEST_SIZE
+    rng = np.random.default_rng(31 + alg)
+    area_t = torch.empty(8 << 20, dtype=torch.uint8, pin_memory=True)
+    area = area_t.numpy()
+    area[:] = rng.integers(0, 256, area.size, dtype=np.uint8)
+    n = 6000
+    lens = rng.integers(0, 1600, n)
+    offs = rng.integers(0, area.size - 1600, n)
+    lens[:4] = (0, 1, 64, 1599)
+    offs[:4] = (0, area.size - 1, area.size - 64, area.size - 1599)   # ends exactly at the area's end
+    pkts = [area[o:o + l] for o, l in zip(offs, lens)]
+    want = _oracle_digests(oracle, alg, [p.copy() for p in pkts], key)
+    got = np.zeros((n, DIGEST_SIZE[alg]), np.uint8)
+    with HashQueue(alg, key=key, max_batch_msgs=500, max_batch_bytes=1 << 20, batches=3) as q:
+        q.register(area_t)
+        def producer(t):
+            for i in range(t, n, 4):
+                q.submit(pkts[i], out=got[i], zerocopy=(i % 5 != 0))
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(4)]
+        [x.start() for x in th]
+        [x.join() for x in th]
+        q.wait()
+        st = q.stats()
+    assert np.array_equal(got, want)
+    assert st["packets"] == n and st["batches"] >= n // 500
+
+
+@pytest.mark.gpu
+def test_zerocopy_errors(gpu):
+    """EINVAL: zero-copy packet outside every registered area, zero copy with
+    two segments, registering pageable memory; ENOMEM past 16 areas."""
+    import torch
+    from liblcb_amd.queue import HashQueue
+    pinned = torch.empty(1 << 16, dtype=torch.uint8, pin_memory=True)
+    with HashQueue(MD5) as q:
+        with pytest.raises(LcbHashError) as e:
+            q.submit(np.zeros(100, np.uint8), zerocopy=True)      # not registered
+        assert e.value.errno == errno.EINVAL
+        with pytest.raises(LcbHashError) as e:
+            q.register(np.zeros(4096, np.uint8))                  # pageable
+        assert e.value.errno == errno.EINVAL
+        q.register(pinned)
+        a = pinned.numpy()
+        with pytest.raises(LcbHashError) as e:
+            q.submit(np.zeros(10, np.uint8), zerocopy=True)       # still outside
+        assert e.value.errno == errno.EINVAL
+        from liblcb_amd._lib import DONE_CB, Q_F_ZEROCOPY, Seg
+        segs = (Seg * 2)()
+        segs[0].data, segs[0].size = a.ctypes.data, 10
+        segs[1].data, segs[1].size = a.ctypes.data + 10, 10
+        assert lib().lcb_hash_queue_submitv(q._q, segs, 2, None, DONE_CB(), None, Q_F_ZEROCOPY) == errno.EINVAL
+        # the area itself works; a packet running past its end does not
+        out = np.zeros(16, np.uint8)
+        a[:3] = np.frombuffer(b"abc", np.uint8)
+        q.submit(a[:3], out=out, zerocopy=True)
+        q.wait()
+        assert out.tobytes().hex() == "900150983cd24fb0d6963f7d28e17f72"
+        assert lib().lcb_hash_queue_submit(q._q, a.ctypes.data + a.size - 8, 16, None, DONE_CB(), None,
+                                           Q_F_ZEROCOPY) == errno.EINVAL
+        more = [torch.empty(4096, dtype=torch.uint8, pin_memory=True) for _ in range(15)]
+        for m in more:
+            q.register(m)
+        with pytest.raises(LcbHashError) as e:
+            q.register(torch.empty(4096, dtype=torch.uint8, pin_memory=True))
+        assert e.value.errno == errno.ENOMEM
+
+
+@pytest.mark.gpu
+def test_native_producers_zerocopy(gpu, oracle, tmp_path):
+    """tools/queue_bench --zerocopy 1: 8 native producers submit 64K x 1 KiB
+    packets of a registered pinned pool in place; digests == oracle."""
+    import json
+    import os
+    import subprocess
+    from oracle.pyoracle import SEED, gen_stream
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "queue_bench")
+    n, size = 1 << 16, 1024
+    out = tmp_path / "dig.bin"
+    r = subprocess.run([exe, "--alg", str(MD5), "--packets", str(n), "--size", str(size), "--threads", "8",
+                        "--batch-msgs", "4096", "--zerocopy", "1", "--out", str(out)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["zerocopy"] == 1 and res["packets"] == n
+    got = np.fromfile(out, np.uint8).reshape(n, 16)
+    want = oracle.batch_fixed_mt(MD5, gen_stream(SEED, n * size), n, size, size)
+    assert np.array_equal(got, want)

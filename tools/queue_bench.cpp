@@ -13,7 +13,12 @@
 // usage: queue_bench [--alg 1] [--packets 1048576] [--size 1024] [--threads 8]
 //                    [--flush-us 200] [--batch-msgs 65536] [--batch-bytes 67108864]
 //                    [--slots 4] [--align 16] [--key HEX] [--cb 1] [--pool-mib 0] [--out FILE]
-//                    [--rate PACKETS_PER_S]
+//                    [--rate PACKETS_PER_S] [--zerocopy 1]
+//
+// --zerocopy: the pool is page-locked (hipHostRegister) and registered with
+// the queue (lcb_hash_queue_register); packets are submitted with
+// LCB_HASH_Q_F_ZEROCOPY, so the queue records (address, length) and the
+// kernel reads them from host memory in place -- no producer memcpy.
 //
 // --rate: open loop.  Producer t's k-th packet is due at t0 + (k * threads + t)
 // / rate (an aggregate rate of `rate`); a producer spins until it is due and the
@@ -34,6 +39,8 @@
 #include <vector>
 
 #include <emmintrin.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../include/lcb_hash_gpu.h"
 #include "../include/lcb_hash_queue.h"
@@ -76,6 +83,7 @@ int main(int argc, char** argv) {
     bool copy_only = false;  // baseline: producers only memcpy into a private arena
     uint64_t pool_mib = 0;  // 0: every packet distinct (cold source); else cycle a pool this big
     double rate = 0;        // packets/s offered (open loop); 0: as fast as possible
+    bool zerocopy = false;  // submit from a registered page-locked pool, no copy
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string a = argv[i], v = argv[i + 1];
         if (a == "--alg") alg = atoi(v.c_str());
@@ -93,6 +101,7 @@ int main(int argc, char** argv) {
         else if (a == "--pool-mib") pool_mib = strtoull(v.c_str(), nullptr, 0);
         else if (a == "--copy-only") copy_only = atoi(v.c_str()) != 0;
         else if (a == "--rate") rate = atof(v.c_str());
+        else if (a == "--zerocopy") zerocopy = atoi(v.c_str()) != 0;
         else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
     const size_t D = lcb_hash_digest_size(alg);
@@ -116,6 +125,12 @@ int main(int argc, char** argv) {
             });
         for (auto& x : th) x.join();
     }
+    if (zerocopy && hipHostRegister(pool.data(), pool.size(), hipHostRegisterDefault) != hipSuccess) {
+        fprintf(stderr, "hipHostRegister failed\n");
+        return 1;
+    }
+    const uint32_t sflags = zerocopy ? LCB_HASH_Q_F_ZEROCOPY : 0u;
+    auto attach = [&](lcb_hash_queue_p qq) { return zerocopy ? lcb_hash_queue_register(qq, pool.data(), pool.size()) : 0; };
     std::vector<uint8_t> digests(packets * D);
     std::vector<int64_t> t_sub(packets), t_done(packets);
     std::atomic<uint64_t> errors{0};
@@ -147,6 +162,7 @@ int main(int argc, char** argv) {
     lcb_hash_queue_p q = nullptr;
     const uint8_t* kp = key.empty() && keyhex.empty() ? nullptr : key.data();
     int rc = lcb_hash_queue_create(alg, kp, key.size(), &cfg, &q);
+    if (!rc) rc = attach(q);
     if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
 
     // Warm-up on a throwaway queue: batches through the whole pipeline (first
@@ -154,11 +170,12 @@ int main(int argc, char** argv) {
     {
         std::vector<uint8_t> wd(std::min<uint64_t>(packets, 16384) * D);
         for (uint64_t i = 0; i < wd.size() / D; ++i)
-            lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &wd[i * D], nullptr, nullptr, 0);
+            lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &wd[i * D], nullptr, nullptr, sflags);
         lcb_hash_queue_wait(q);
         lcb_hash_queue_destroy(q);
         q = nullptr;
         rc = lcb_hash_queue_create(alg, kp, key.size(), &cfg, &q);
+        if (!rc) rc = attach(q);
         if (rc) { fprintf(stderr, "create: %s\n", lcb_hash_strerror(rc)); return 1; }
     }
     lcb_hash_queue_stats_t st0;
@@ -180,7 +197,7 @@ int main(int argc, char** argv) {
                         while (now_ns() < due) _mm_pause();
                         t_sub[i] = due;
                         int r = lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &digests[i * D],
-                                                      use_cb ? on_done : nullptr, (void*)(uintptr_t)i, 0);
+                                                      use_cb ? on_done : nullptr, (void*)(uintptr_t)i, sflags);
                         if (r) { fail.store(r); return; }
                     }
                     return;
@@ -189,7 +206,7 @@ int main(int argc, char** argv) {
                 for (uint64_t i = lo; i < hi; ++i) {
                     t_sub[i] = now_ns();
                     int r = lcb_hash_queue_submit(q, &pool[(i % pool_pk) * size], size, &digests[i * D],
-                                                  use_cb ? on_done : nullptr, (void*)(uintptr_t)i, 0);
+                                                  use_cb ? on_done : nullptr, (void*)(uintptr_t)i, sflags);
                     if (r) { fail.store(r); return; }
                 }
             });
@@ -214,7 +231,7 @@ int main(int argc, char** argv) {
     const uint64_t worst = std::max_element(lat.begin(), lat.end()) - lat.begin();
     std::sort(lat.begin(), lat.end());
     const double sec = (t1 - t0) * 1e-9;
-    printf("{\"alg\": %d, \"rate\": %.0f, \"lat_us_p999\": %.1f, \"late_half_p99\": %.1f, \"late_half_max\": %.1f, "
+    printf("{\"alg\": %d, \"zerocopy\": %d, \"rate\": %.0f, \"lat_us_p999\": %.1f, \"late_half_p99\": %.1f, \"late_half_max\": %.1f, "
            "\"worst_at\": %.4f, \"packets\": %llu, \"size\": %llu, \"threads\": %d, \"flush_usec\": %u, "
            "\"batch_msgs\": %llu, \"batch_bytes\": %llu, \"slots\": %u, \"pool_mib\": %llu, \"seconds\": %.4f, "
            "\"packets_per_s\": %.0f, \"GiB_s\": %.3f, \"lat_us_p50\": %.1f, \"lat_us_p99\": %.1f, "
@@ -222,7 +239,7 @@ int main(int argc, char** argv) {
            "\"sealed_flush\": %llu, \"submit_waits\": %llu, \"cb\": %d, \"drain_ms\": %.2f, \"launch_ms\": %.2f, "
            "\"completer_busy_ms\": %.2f, \"gpu_wait_ms\": %.2f, \"max_fill_us\": %.1f, \"max_launch_us\": %.1f, "
            "\"max_gpu_us\": %.1f, \"max_callback_us\": %.1f, \"max_submit_wait_us\": %.1f}\n",
-           alg, rate, lat[packets * 999 / 1000], lat2[lat2.size() * 99 / 100], lat2.back(), (double)worst / packets,
+           alg, (int)zerocopy, rate, lat[packets * 999 / 1000], lat2[lat2.size() * 99 / 100], lat2.back(), (double)worst / packets,
            (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
            (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, (unsigned long long)pool_mib, sec,
            packets / sec, nbytes / sec / (1ull << 30), lat[packets / 2], lat[packets * 99 / 100],
