@@ -216,24 +216,38 @@ __global__ __launch_bounds__(256) void gost_hmac_prep_kernel(KeyBlock kb, const 
     st.save(mid + kMidWords, T);
 }
 
-static dim3 gost_grid(uint64_t count) {
+// Persistent grid: as many workgroups as fit on the chip at once (the LDS of
+// the image + Sigma and the VGPRs decide how many per CU).
+template <class K>
+static dim3 gost_grid(K kern, uint64_t count) {
     const uint64_t need = (count + kGostThreads - 1) / kGostThreads;
-    const uint64_t cus = (uint64_t)device_cu_count();
-    return dim3((unsigned)(need < cus ? need : cus));
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kGostThreads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    const uint64_t slots = (uint64_t)per_cu * device_cu_count();
+    return dim3((unsigned)(need < slots ? need : slots));
 }
 template <bool k256>
 void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
-    const dim3 g = gost_grid(a.count);
-    if (hmac) hipLaunchKernelGGL((gost_batch_kernel<k256, true>), g, dim3(kGostThreads), 0, s, a);
-    else hipLaunchKernelGGL((gost_batch_kernel<k256, false>), g, dim3(kGostThreads), 0, s, a);
+    if (hmac) {
+        auto k = gost_batch_kernel<k256, true>;
+        hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
+    } else {
+        auto k = gost_batch_kernel<k256, false>;
+        hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
+    }
+}
+template <bool k256, int kMode>
+static void launch_gost_keyed_mode(const KArgs& a, hipStream_t s) {
+    auto k = gost_keyed_kernel<k256, kMode>;
+    hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
 }
 template <bool k256>
 void launch_gost_keyed(const KArgs& a, hipStream_t s) {
-    const dim3 g = gost_grid(a.count);
     switch (a.key_mode) {
-    case kKeyHmac: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyHmac>), g, dim3(kGostThreads), 0, s, a); break;
-    case kKeyPrefix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeyPrefix>), g, dim3(kGostThreads), 0, s, a); break;
-    case kKeySuffix: hipLaunchKernelGGL((gost_keyed_kernel<k256, kKeySuffix>), g, dim3(kGostThreads), 0, s, a); break;
+    case kKeyHmac: launch_gost_keyed_mode<k256, kKeyHmac>(a, s); break;
+    case kKeyPrefix: launch_gost_keyed_mode<k256, kKeyPrefix>(a, s); break;
+    case kKeySuffix: launch_gost_keyed_mode<k256, kKeySuffix>(a, s); break;
     }
 }
 

@@ -52,6 +52,9 @@
 
 namespace lcbgpu {
 
+#ifndef LCB_TILE_NODMA
+#define LCB_TILE_NODMA 0
+#endif
 enum { kTilePlain = 0, kTileHmac = 1, kTileKeyedHmac = 2, kTileKeyedSuffix = 3 };
 
 constexpr int kTileWaves = 4;     // waves per workgroup (one 8 KiB slab each)
@@ -161,8 +164,12 @@ __device__ __forceinline__ void tile_assemble(uint32_t Q, const uint32_t* c, con
 // literals (Md5::addk), other hashes as they are.
 template <class H>
 __device__ __forceinline__ void tile_compress(H& st, const uint32_t* w) {
-    if constexpr (std::is_same<H, Md5>::value) st.template compress<true>(w);
+#if LCB_TILE_NOCOMP
+    st.s[0] ^= w[0] + w[5]; st.s[1] ^= w[9] + w[15];
+#else
+    if constexpr (std::is_same<H, Md5>::value) st.compress_asm(w);
     else st.compress(w);
+#endif
 }
 
 // Block b of a lane's (virtual) message from the streamed words w: whole
@@ -292,10 +299,14 @@ struct TileGatherStream {
         uint64_t so = (uint64_t)L * 128u;
         asm volatile("" : "+s"(so));
         const uint8_t* sb = tb + so;
+#if !LCB_TILE_NODMA
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g]),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
+#else
+        (void)sb;
+#endif
     }
     // lastc: index of this lane's last stream chunk holding a record byte.
     template <int kAux>
@@ -314,6 +325,7 @@ struct TileGatherStream {
         for (int g = 0; g < 8; ++g) {
             const uint32_t k = (ln & 7u) ^ (uint32_t)g;
             const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
+            if (LCB_TILE_NODMA) continue;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
         }
@@ -458,7 +470,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 template <class H, int kMode>
 __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nwaves) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kTileWaves][8192];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // Wave index as a scalar: the slab base (every DMA's M0) stays in SGPRs.
+    const uint32_t lane = threadIdx.x & 63, wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
     const uint64_t ntiles = (norder + 63) / 64;
     TileClaim cl;

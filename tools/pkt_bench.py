@@ -36,6 +36,35 @@ def ragged_1k(stride, steps):
             "TB_s": round(count * 1024 / (ms * 1e-3) / 1e12, 3)}
 
 
+def packets_layout(kind, steps):
+    """The packet lengths (tests/golden_util.packet_layout) in other layouts:
+    `sorted` packs them in descending length order (a tile's records lie
+    close together in memory), `aligned128` starts every packet on a 128-B
+    line (no streamed line straddles two cache lines)."""
+    from tests.golden_util import packet_layout
+    _, lens, _ = packet_layout()
+    lens = lens.astype(np.uint64)
+    if kind == "sorted":
+        lens = np.sort(lens)[::-1].copy()
+    span = (lens + 127) // 128 * 128 if kind == "aligned128" else lens
+    offs = np.zeros(len(lens), np.uint64)
+    offs[1:] = np.cumsum(span[:-1], dtype=np.uint64)
+    total = int(offs[-1] + span[-1])
+    count = len(lens)
+    data = liblcb_amd.gen_synthetic(bench.SEED, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    dig = torch.empty((count, 16), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def launch():
+        check(lib().lcb_hash_batch(1, None, 0, data.data_ptr(), do.data_ptr(), dl.data_ptr(), count, 0, 0,
+                                   dig.data_ptr(), F_DEVICE, s.cuda_stream))
+    ms = bench._event_ms(launch, 10, steps, s)
+    nbytes = int(lens.sum())
+    return {"variant": "packets_" + kind, "ms": round(ms, 4), "TB_s": round(nbytes / (ms * 1e-3) / 1e12, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -45,6 +74,8 @@ def main():
     torch.cuda.set_device(0)
     bench.settle()
     print(json.dumps({"ragged_packets": bench.bench_packets(10, a.steps, tuple(a.algs.split(",")))}), flush=True)
+    for kind in ("sorted", "aligned128"):
+        print(json.dumps(packets_layout(kind, a.steps)), flush=True)
     for st in (1024, 1040, 1025):
         print(json.dumps(ragged_1k(st, a.steps)), flush=True)
     if not a.no_c4:
