@@ -9,9 +9,9 @@ mkdir -p $OUT
 cd $R
 V=${VARIANTS:-md5asm}
 lib() { [ $1 = product ] && echo liblcb_amd/liblcb_hash_gpu.so || echo build_exp/$1/liblcb_hash_gpu.so; }
-first=${V%% *}
+first=${PYTEST_VARIANT:-product}
 if [ -z "$SKIP_PYTEST" ]; then
-LCB_HASH_GPU_LIB=$(lib $first) timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_packets.py tests/test_radius_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_$first.log 2>&1
+LCB_HASH_GPU_LIB=$(lib $first) timeout -k 10 300 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_$first.log 2>&1
 rc=$?; echo "pytest $first rc=$rc"; tail -2 $OUT/pytest_$first.log; [ $rc -ne 0 ] && exit $rc
 fi
 [ -n "$LIST_COUNTERS" ] && (cd /tmp && TMPDIR=/tmp timeout -k 5 60 rocprofv3 -L > $OUT/counters.txt 2>&1)
