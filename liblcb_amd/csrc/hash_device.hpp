@@ -333,102 +333,6 @@ struct Md5 {
         s[0] += a; s[1] += b; s[2] += c; s[3] += d;
     }
 #undef LCB_MD5_STEP
-    // The 64 steps as ONE asm statement (T as inline literals).  On gfx950
-    // the compiler's hazard recogniser assumes every inline-asm VGPR result
-    // carries the dst-sel forwarding hazard and puts an `s_nop 0` in front of
-    // any VALU (or asm) that reads it next; an `s_nop 0` costs a SIMD 4 issue
-    // cycles like a VALU instruction (MI355X_MICROARCH.md), so the per-step
-    // addk form above paid one nop per 5 VALU.  Inside one statement the
-    // plain 32-bit VOP2/VOP3 writes carry no such hazard; only the state's
-    // consumers after the block see one nop.  Used by the ragged tile kernel
-    // (packets 0.680 -> 0.664 ms); the fixed-stride kernel keeps the per-step
-    // form, which measured 2-4 % faster there (power-limited clock;
-    // profiles/r3_md5_form_ab.txt).
-#define LCB_M5(F, a, a0, b, c, d, x, T, s)                                                        \
-    "v_bitop3_b32 %[t], %[" #b "], %[" #c "], %[" #d "] bitop3:" #F "\n\t"                        \
-    "v_add3_u32 %[" #a "], %[" #a0 "], %[t], %[w" #x "]\n\t"                                      \
-    "v_add_u32_e32 %[" #a "], " #T ", %[" #a "]\n\t"                                              \
-    "v_alignbit_b32 %[" #a "], %[" #a "], %[" #a "], " #s "\n\t"                                  \
-    "v_add_u32_e32 %[" #a "], %[" #a "], %[" #b "]\n\t"
-    // F1 = ch(b,c,d) 0xca; F2 = (b & d) | (c & ~d) 0xe4; F3 = b ^ c ^ d 0x96;
-    // F4 = c ^ (b | ~d) 0x39 (truth tables over b = 0xf0, c = 0xcc, d = 0xaa).
-    // Rotate left by r = v_alignbit by 32 - r.
-    __device__ __forceinline__ void compress_asm(const uint32_t* w) {
-        uint32_t a, b, c, d, t;   // steps 1-4 read the entry state s[] directly
-        asm(
-            LCB_M5(0xca, a, s0, s1, s2, s3, 0, 0xd76aa478, 25)
-            LCB_M5(0xca, d, s3, a, s1, s2, 1, 0xe8c7b756, 20)
-            LCB_M5(0xca, c, s2, d, a, s1, 2, 0x242070db, 15)
-            LCB_M5(0xca, b, s1, c, d, a, 3, 0xc1bdceee, 10)
-            LCB_M5(0xca, a, a, b, c, d, 4, 0xf57c0faf, 25)
-            LCB_M5(0xca, d, d, a, b, c, 5, 0x4787c62a, 20)
-            LCB_M5(0xca, c, c, d, a, b, 6, 0xa8304613, 15)
-            LCB_M5(0xca, b, b, c, d, a, 7, 0xfd469501, 10)
-            LCB_M5(0xca, a, a, b, c, d, 8, 0x698098d8, 25)
-            LCB_M5(0xca, d, d, a, b, c, 9, 0x8b44f7af, 20)
-            LCB_M5(0xca, c, c, d, a, b, 10, 0xffff5bb1, 15)
-            LCB_M5(0xca, b, b, c, d, a, 11, 0x895cd7be, 10)
-            LCB_M5(0xca, a, a, b, c, d, 12, 0x6b901122, 25)
-            LCB_M5(0xca, d, d, a, b, c, 13, 0xfd987193, 20)
-            LCB_M5(0xca, c, c, d, a, b, 14, 0xa679438e, 15)
-            LCB_M5(0xca, b, b, c, d, a, 15, 0x49b40821, 10)
-            LCB_M5(0xe4, a, a, b, c, d, 1, 0xf61e2562, 27)
-            LCB_M5(0xe4, d, d, a, b, c, 6, 0xc040b340, 23)
-            LCB_M5(0xe4, c, c, d, a, b, 11, 0x265e5a51, 18)
-            LCB_M5(0xe4, b, b, c, d, a, 0, 0xe9b6c7aa, 12)
-            LCB_M5(0xe4, a, a, b, c, d, 5, 0xd62f105d, 27)
-            LCB_M5(0xe4, d, d, a, b, c, 10, 0x02441453, 23)
-            LCB_M5(0xe4, c, c, d, a, b, 15, 0xd8a1e681, 18)
-            LCB_M5(0xe4, b, b, c, d, a, 4, 0xe7d3fbc8, 12)
-            LCB_M5(0xe4, a, a, b, c, d, 9, 0x21e1cde6, 27)
-            LCB_M5(0xe4, d, d, a, b, c, 14, 0xc33707d6, 23)
-            LCB_M5(0xe4, c, c, d, a, b, 3, 0xf4d50d87, 18)
-            LCB_M5(0xe4, b, b, c, d, a, 8, 0x455a14ed, 12)
-            LCB_M5(0xe4, a, a, b, c, d, 13, 0xa9e3e905, 27)
-            LCB_M5(0xe4, d, d, a, b, c, 2, 0xfcefa3f8, 23)
-            LCB_M5(0xe4, c, c, d, a, b, 7, 0x676f02d9, 18)
-            LCB_M5(0xe4, b, b, c, d, a, 12, 0x8d2a4c8a, 12)
-            LCB_M5(0x96, a, a, b, c, d, 5, 0xfffa3942, 28)
-            LCB_M5(0x96, d, d, a, b, c, 8, 0x8771f681, 21)
-            LCB_M5(0x96, c, c, d, a, b, 11, 0x6d9d6122, 16)
-            LCB_M5(0x96, b, b, c, d, a, 14, 0xfde5380c, 9)
-            LCB_M5(0x96, a, a, b, c, d, 1, 0xa4beea44, 28)
-            LCB_M5(0x96, d, d, a, b, c, 4, 0x4bdecfa9, 21)
-            LCB_M5(0x96, c, c, d, a, b, 7, 0xf6bb4b60, 16)
-            LCB_M5(0x96, b, b, c, d, a, 10, 0xbebfbc70, 9)
-            LCB_M5(0x96, a, a, b, c, d, 13, 0x289b7ec6, 28)
-            LCB_M5(0x96, d, d, a, b, c, 0, 0xeaa127fa, 21)
-            LCB_M5(0x96, c, c, d, a, b, 3, 0xd4ef3085, 16)
-            LCB_M5(0x96, b, b, c, d, a, 6, 0x04881d05, 9)
-            LCB_M5(0x96, a, a, b, c, d, 9, 0xd9d4d039, 28)
-            LCB_M5(0x96, d, d, a, b, c, 12, 0xe6db99e5, 21)
-            LCB_M5(0x96, c, c, d, a, b, 15, 0x1fa27cf8, 16)
-            LCB_M5(0x96, b, b, c, d, a, 2, 0xc4ac5665, 9)
-            LCB_M5(0x39, a, a, b, c, d, 0, 0xf4292244, 26)
-            LCB_M5(0x39, d, d, a, b, c, 7, 0x432aff97, 22)
-            LCB_M5(0x39, c, c, d, a, b, 14, 0xab9423a7, 17)
-            LCB_M5(0x39, b, b, c, d, a, 5, 0xfc93a039, 11)
-            LCB_M5(0x39, a, a, b, c, d, 12, 0x655b59c3, 26)
-            LCB_M5(0x39, d, d, a, b, c, 3, 0x8f0ccc92, 22)
-            LCB_M5(0x39, c, c, d, a, b, 10, 0xffeff47d, 17)
-            LCB_M5(0x39, b, b, c, d, a, 1, 0x85845dd1, 11)
-            LCB_M5(0x39, a, a, b, c, d, 8, 0x6fa87e4f, 26)
-            LCB_M5(0x39, d, d, a, b, c, 15, 0xfe2ce6e0, 22)
-            LCB_M5(0x39, c, c, d, a, b, 6, 0xa3014314, 17)
-            LCB_M5(0x39, b, b, c, d, a, 13, 0x4e0811a1, 11)
-            LCB_M5(0x39, a, a, b, c, d, 4, 0xf7537e82, 26)
-            LCB_M5(0x39, d, d, a, b, c, 11, 0xbd3af235, 22)
-            LCB_M5(0x39, c, c, d, a, b, 2, 0x2ad7d2bb, 17)
-            LCB_M5(0x39, b, b, c, d, a, 9, 0xeb86d391, 11)
-            : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [t] "=&v"(t)
-            : [s0] "v"(s[0]), [s1] "v"(s[1]), [s2] "v"(s[2]), [s3] "v"(s[3]),
-              [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]), [w4] "v"(w[4]),
-              [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]), [w9] "v"(w[9]),
-              [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]), [w13] "v"(w[13]), [w14] "v"(w[14]),
-              [w15] "v"(w[15]));
-        s[0] += a; s[1] += b; s[2] += c; s[3] += d;
-    }
-#undef LCB_M5
     // md5.h:282: LE u64 bit length in bytes 56..63.
     __device__ __forceinline__ static void put_length(uint32_t* w, uint64_t bytes) {
         const uint64_t bits = bytes << 3;

@@ -62,17 +62,11 @@ struct KeyBlock {
 constexpr int kBucketClasses = 122;
 constexpr int kBucketPhases = 6;
 constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
-// Bucketing scratch ahead of the permutation (uint32 words): key histogram,
-// per-key fill counters, the tile queue's kTileHeads heads (one per XCD, each
-// on its own 128-B line), the number of entries of `order` (pads included).
-#ifndef LCB_TILE_HEADS
-#define LCB_TILE_HEADS 8
-#endif
-constexpr int kTileHeads = LCB_TILE_HEADS;
-constexpr int kTileHeadStride = 32;
-constexpr int kBucketHead = (2 * kBucketKeys + kTileHeadStride - 1) / kTileHeadStride * kTileHeadStride;
-constexpr int kBucketNTiles = kBucketHead + kTileHeads * kTileHeadStride;
-constexpr int kBucketWork = kBucketNTiles + 1;
+// Bucketing scratch ahead of the permutation: key histogram, per-key fill
+// counters, the tile-queue head, the number of 64-entry tiles (uint32 words).
+constexpr int kBucketHead = 2 * kBucketKeys;
+constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
+constexpr int kBucketWork = 2 * kBucketKeys + 2;
 // Ragged batches at least this large are bucketed by length first.
 constexpr uint64_t kBucketMinCount = 4096;
 // When every key has enough messages (count >= kBucketPadRatio * 64 * keys

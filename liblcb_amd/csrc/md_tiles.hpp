@@ -52,9 +52,6 @@
 
 namespace lcbgpu {
 
-#ifndef LCB_TILE_NODMA
-#define LCB_TILE_NODMA 0
-#endif
 enum { kTilePlain = 0, kTileHmac = 1, kTileKeyedHmac = 2, kTileKeyedSuffix = 3 };
 
 constexpr int kTileWaves = 4;     // waves per workgroup (one 8 KiB slab each)
@@ -81,26 +78,14 @@ struct TileRec {
     bool valid;
 };
 
-// The next tile, claimed during the current one in three steps, one per
-// stream line (queue atomic -> order entry -> offset / length), so each round
-// trip is waited for by the line stream's own wait.  Eight queue heads, one
-// per XCD (workgroup i runs on XCD i mod 8), each on its own 128-B line: one
-// device-scope word saturates at ~88 dequeues per us (MI355X_MICROARCH.md,
-// dequeue), and every XCD's waves pulled from one.  Head x hands out tiles
-// nwaves + 8 k + x, so the heads walk the longest-first order side by side.
+// The next tile, claimed near the end of the current one in three steps, one
+// per stream line, so the dependent round trips (queue atomic -> order entry
+// -> offset / length) are waited for by the line stream's own waits.
 struct TileClaim {
     uint64_t t;      // tile (wave-uniform)
     uint32_t ent;    // this lane's order entry
     TileRec r;
     int stage;       // 0: nothing yet, 1: t, 2: ent, 3: r
-};
-
-// The queue a wave pulls from.
-struct TileQueue {
-    uint64_t ntiles;
-    uint32_t norder;   // entries of `order`, pads included
-    uint32_t nwaves;   // static first tiles
-    uint32_t head;     // this workgroup's head (blockIdx.x & 7)
 };
 
 __device__ __forceinline__ void tile_rec_load(const KArgs& a, uint32_t ent, TileRec& r) {
@@ -116,15 +101,17 @@ __device__ __forceinline__ uint32_t tile_entry(const KArgs& a, uint64_t t, uint3
     return i < norder ? gptr(a.order)[i] : kOrderPad;
 }
 
-__device__ __forceinline__ void tile_claim_step(const KArgs& a, TileClaim& c, uint32_t lane, const TileQueue& q) {
+// One step of the claim.  nwaves: first queue ticket = the static tiles.
+__device__ __forceinline__ void tile_claim_step(const KArgs& a, TileClaim& c, uint32_t lane, uint64_t ntiles,
+                                                uint32_t norder, uint32_t nwaves) {
     if (c.stage == 0) {
         uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(a.tile_next + kTileHeadStride * q.head, 1u);   // device scope, old head
-        c.t = (uint64_t)q.nwaves + (uint64_t)kTileHeads * (uint32_t)__builtin_amdgcn_readfirstlane(v) + q.head;
+        if (lane == 0) v = atomicAdd(a.tile_next, 1u);   // device scope, returns the old head
+        c.t = (uint64_t)nwaves + (uint32_t)__builtin_amdgcn_readfirstlane(v);
     } else if (c.stage == 1) {
-        if (c.t < q.ntiles) c.ent = tile_entry(a, c.t, lane, q.norder);
+        if (c.t < ntiles) c.ent = tile_entry(a, c.t, lane, norder);
     } else if (c.stage == 2) {
-        if (c.t < q.ntiles) tile_rec_load(a, c.ent, c.r);
+        if (c.t < ntiles) tile_rec_load(a, c.ent, c.r);
     }
     ++c.stage;
 }
@@ -156,9 +143,11 @@ __device__ __forceinline__ void tile_shift(const uint32_t* c, const uint32_t* y,
         }
     }
 }
-// Dispatch on the tile's (wave-uniform) Q.
+// Dispatch on the tile's (wave-uniform) Q.  Q passes through an empty asm at
+// every call so the compiler does not clone the whole line loop per Q.
 __device__ __forceinline__ void tile_assemble(uint32_t Q, const uint32_t* c, const uint32_t* y, uint32_t sh,
                                               uint32_t w[16]) {
+    asm volatile("" : "+s"(Q));
     switch (Q) {
     case 0: tile_shift<0>(c, y, sh, w); break;
     case 1: tile_shift<1>(c, y, sh, w); break;
@@ -172,12 +161,8 @@ __device__ __forceinline__ void tile_assemble(uint32_t Q, const uint32_t* c, con
 // literals (Md5::addk), other hashes as they are.
 template <class H>
 __device__ __forceinline__ void tile_compress(H& st, const uint32_t* w) {
-#if LCB_TILE_NOCOMP
-    st.s[0] ^= w[0] + w[5]; st.s[1] ^= w[9] + w[15];
-#else
-    if constexpr (std::is_same<H, Md5>::value) st.compress_asm(w);
+    if constexpr (std::is_same<H, Md5>::value) st.template compress<true>(w);
     else st.compress(w);
-#endif
 }
 
 // Block b of a lane's (virtual) message from the streamed words w: whole
@@ -307,14 +292,10 @@ struct TileGatherStream {
         uint64_t so = (uint64_t)L * 128u;
         asm volatile("" : "+s"(so));
         const uint8_t* sb = tb + so;
-#if !LCB_TILE_NODMA
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g]),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
-#else
-        (void)sb;
-#endif
     }
     // lastc: index of this lane's last stream chunk holding a record byte.
     template <int kAux>
@@ -333,7 +314,6 @@ struct TileGatherStream {
         for (int g = 0; g < 8; ++g) {
             const uint32_t k = (ln & 7u) ^ (uint32_t)g;
             const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
-            if (LCB_TILE_NODMA) continue;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
         }
@@ -356,41 +336,23 @@ struct TileGatherStream {
     }
 };
 
-// A tile's wave-uniform geometry, computed from its 64 records once they are
-// loaded (for the next tile: while the current one streams its last lines).
-// The tile's phase: Q = 16 for a record on the second half of a 128-B line,
-// 0 on its first half (both: the stream is whole cache lines), else the
-// start's dword inside its 16-B chunk; the stream base of a record is its
-// start minus off0 (64, or its byte offset inside its 16-B chunk).
-struct TileGeom {
-    uint64_t lo;       // lowest stream base of the tile
-    uint32_t Q;
-    uint32_t NL;       // lines holding record bytes (max over the wave)
-    uint32_t NS;       // lines wholly inside every record (min)
-    uint32_t NB;       // blocks of the padded message (max; plain / HMAC)
-    uint32_t NF;       // whole message blocks (min)
-    uint32_t LE;       // lines streamed (keyed suffix: only the whole-block lines)
-    bool wl;           // whole cache lines: the nt policy
-    bool stream;       // else the per-lane loop
-};
-
-__device__ __forceinline__ uint32_t tile_off0(const TileRec& r, uint32_t Q) {
-    return Q == 16 ? 64u : ((uint32_t)reinterpret_cast<uintptr_t>(r.p) & 15u);
-}
-
-template <int kMode>
-__device__ __forceinline__ void tile_geom(const TileRec& r, TileGeom& g) {
+template <class H, int kMode>
+__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
+                                               uint32_t Q, bool whole_lines, TileClaim& cl, uint64_t ntiles,
+                                               uint32_t norder, uint32_t nwaves) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
-    const bool wl = (p32 & 63u) == 0;
-    const uint32_t Ql = wl ? ((p32 & 64u) ? 16u : 0u) : ((p32 >> 2) & 3u);
-    const uint32_t Q = (uint32_t)__builtin_amdgcn_readfirstlane(Ql);
-    const bool uniform = __all(Ql == Q);
-    g.Q = Q;
-    g.wl = __all(wl);
-    const uint32_t off0 = tile_off0(r, Q);
-    const uint64_t end = off0 + (uint64_t)r.len;              // record end, in stream bytes
-    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7);
-    uint32_t NB = (uint32_t)(((uint64_t)r.len + 8u) >> 6) + 1u, NF = r.len >> 6;
+    const uint32_t sh = p32 & 3u;
+    // Stream offset of the record's first byte: base = p - off0.
+    const uint32_t off0 = Q == 16 ? 64u : (p32 & 15u);
+    const uint64_t len = r.len;
+    H st;
+    TileMsg<H, kMode> m;
+    tile_state(a, r, st, m);
+    // Geometry: lines holding record bytes, lines wholly inside every record,
+    // blocks of the padded (virtual) message, whole message blocks.
+    const uint64_t end = off0 + len;                        // record end, in stream bytes
+    const uint32_t nblk = (uint32_t)((m.total + 8u) >> 6) + 1u;
+    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7), NB = nblk, NF = r.len >> 6;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {                       // wave max / min (xor butterfly)
         NL = max(NL, (uint32_t)__shfl_xor((int)NL, d, 64));
@@ -398,12 +360,12 @@ __device__ __forceinline__ void tile_geom(const TileRec& r, TileGeom& g) {
         NS = min(NS, (uint32_t)__shfl_xor((int)NS, d, 64));
         NF = min(NF, (uint32_t)__shfl_xor((int)NF, d, 64));
     }
-    g.NL = __builtin_amdgcn_readfirstlane(NL);
-    g.NB = __builtin_amdgcn_readfirstlane(NB);
-    g.NS = __builtin_amdgcn_readfirstlane(NS);
-    g.NF = __builtin_amdgcn_readfirstlane(NF);
-    // Stream bases as 32-bit offsets from the lowest (saddr form): the tile
-    // must span less than 4 GiB, else the per-lane loop.
+    NL = __builtin_amdgcn_readfirstlane(NL);
+    NB = __builtin_amdgcn_readfirstlane(NB);
+    NS = __builtin_amdgcn_readfirstlane(NS);
+    NF = __builtin_amdgcn_readfirstlane(NF);
+    // The tile's stream bases: 32-bit offsets from the lowest (saddr form)
+    // when the tile spans less than 4 GiB, else the per-lane loop.
     const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off0;
     uint64_t lo = base, hi = base;
 #pragma unroll
@@ -411,95 +373,43 @@ __device__ __forceinline__ void tile_geom(const TileRec& r, TileGeom& g) {
         lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d, 64));
         hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d, 64));
     }
-    g.lo = readfirstlane64(lo);
+    lo = readfirstlane64(lo);
     hi = readfirstlane64(hi);
-    // Keyed suffix: the stream carries the whole-block lines only, the rest
-    // (under two lines of message, then the key) goes through the per-lane
-    // loop: the key's window assembly next to a streamed line needs more
-    // VGPRs than the occupancy leaves.
-    const uint32_t LF = (g.NF + 1) / 2 < g.NL ? (g.NF + 1) / 2 : g.NL;
-    g.LE = kMode == kTileKeyedSuffix ? LF : g.NL;
-    g.stream = uniform && hi - g.lo + (uint64_t)(g.NL + 1) * 128u < (1ull << 32) && __all(end != 0) && g.LE > 0;
-}
-
-// Line L of a streaming tile into the slab: the nt policy for whole cache
-// lines, masked chunks from the first line not wholly inside every record.
-__device__ __forceinline__ void tile_issue(TileGatherStream& ls, const TileGeom& g, uint32_t L, uint32_t lastc) {
-    if (L >= g.NS) {
-        if (g.wl) ls.issue_masked<kLdsAux>(L, lastc);
-        else ls.issue_masked<kGatherAux>(L, lastc);
-    } else {
-        if (g.wl) ls.issue<kLdsAux>(L);
-        else ls.issue<kGatherAux>(L);
+    if (hi - lo + (uint64_t)(NL + 1) * 128u >= (1ull << 32) || !__all(end != 0)) {
+        if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m.K, m.kl, 0);
+        else md_message(st, r.p, r.len, m.prefix);
+        tile_finish<H, kMode>(a, st, r);
+        return;
     }
-}
-
-// The next tile, in two steps.  tile_prep_geom, once the current tile has
-// issued its last line (its stream offsets are dead then): finish the claim,
-// compute the next tile's geometry and stream offsets.  tile_prep_issue,
-// once the current tile has taken its last line (the slab is free): issue
-// the next tile's line 0, so it is in flight while the current tile
-// computes its last lines.  cl.t >= ntiles: no next tile.
-template <int kMode>
-__device__ __forceinline__ void tile_prep_geom(const KArgs& a, TileClaim& cl, const TileQueue& q, uint32_t lane,
-                                               uint8_t* slab, TileGatherStream& ls, TileGeom& gn, uint32_t& lastc_n) {
-    while (cl.stage < 3) tile_claim_step(a, cl, lane, q);
-    gn.stream = false;
-    if (cl.t < q.ntiles) {
-        tile_geom<kMode>(cl.r, gn);
-        if (gn.stream) {
-            const uint32_t off0 = tile_off0(cl.r, gn.Q);
-            const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(cl.r.p) - off0;
-            ls.init(reinterpret_cast<const uint8_t*>(gn.lo), (uint32_t)(base - gn.lo), lane, slab);
-            lastc_n = (uint32_t)((off0 + (uint64_t)cl.r.len - 1) >> 4);
-        }
-    }
-}
-__device__ __forceinline__ void tile_prep_issue(TileGatherStream& ls, const TileGeom& gn, uint32_t lastc_n) {
-    if (gn.stream) tile_issue(ls, gn, 0, lastc_n);
-}
-
-// A streaming tile whose line 0 is in flight.
-template <class H, int kMode>
-__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, const TileGeom& g, uint32_t lane,
-                                               uint8_t* slab, TileGatherStream& ls, TileClaim& cl,
-                                               const TileQueue& q, TileGeom& gn) {
-    const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
-    const uint32_t sh = p32 & 3u;
-    const uint32_t Q = g.Q;
-    const uint64_t len = r.len;
-    const uint64_t end = tile_off0(r, Q) + len;               // record end, in stream bytes
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
-    uint32_t lastc_n = 0;                                     // the next tile's, for its line 0
-    H st;
-    TileMsg<H, kMode> m;
-    tile_state(a, r, st, m);
-    const uint32_t nblk = (uint32_t)((m.total + 8u) >> 6) + 1u;
-    const uint32_t NL = g.NL, NB = g.NB, NF = g.NF, LE = g.LE;
-    // Claim steps on the lines before the next tile's set-up (tile_prep_geom
-    // at the end of line LE - 2, or before line 0 for a one-line stream).
-    const uint32_t c0 = LE > 5 ? LE - 5 : 0u;
-    if (LE == 1) tile_prep_geom<kMode>(a, cl, q, lane, slab, ls, gn, lastc_n);
-    auto after_take = [&](uint32_t L) {
-        if (L + 1 < LE) {
-            tile_issue(ls, g, L + 1, lastc);
-            if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, q);
-        } else if (L + 1 == LE) {
-            tile_prep_issue(ls, gn, lastc_n);
+    TileGatherStream ls;
+    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(base - lo), lane, slab);
+    auto issue = [&](uint32_t L) {
+        if (L >= NS) {
+            if (whole_lines) ls.issue_masked<kLdsAux>(L, lastc);
+            else ls.issue_masked<kGatherAux>(L, lastc);
+        } else {
+            if (whole_lines) ls.issue<kLdsAux>(L);
+            else ls.issue<kGatherAux>(L);
         }
     };
-    auto line_end = [&](uint32_t L) {
-        if (L + 2 == LE) tile_prep_geom<kMode>(a, cl, q, lane, slab, ls, gn, lastc_n);
-    };
+    const uint32_t c0 = NL > 3 ? NL - 3 : 0u;                // first claim step
+    if (NL) issue(0);
     uint32_t c[16];   // dwords 16..31 of the previous line (the carry)
     // Whole-block lines: both blocks of line L (2L - 1 and 2L) are whole
     // message blocks of every lane (2L < NF).
     const uint32_t LF = (NF + 1) / 2 < NL ? (NF + 1) / 2 : NL;
+    // Keyed suffix: the stream ends with the whole-block lines, the rest
+    // (under two lines of message, the key) goes through the per-lane loop:
+    // the key's window assembly next to a streamed line needs more VGPRs
+    // than the occupancy leaves.
+    const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
     uint32_t L = 0;
     for (; L < LF; ++L) {
         uint32_t y[32];
         ls.take(y);
-        after_take(L);
+        if (L + 1 < LE) issue(L + 1);
+        if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         uint32_t w[16];
         if (L > 0) {   // block 2L - 1: the carry and dwords 0..Q of this line
             tile_assemble(Q, c, y, sh, w);
@@ -509,10 +419,10 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         tile_compress(st, w);
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
-        line_end(L);
     }
     if constexpr (kMode == kTileKeyedSuffix) {
         const uint64_t done = LF ? (2ull * LF - 1) * 64u : 0u;   // blocks 0 .. 2 LF - 2
+        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         md_message2(st, r.p + done, len - done, m.K, m.kl, m.prefix + done);
         tile_finish<H, kMode>(a, st, r);
         return;
@@ -524,7 +434,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         uint32_t y[32];
         if (L < NL) {
             ls.take(y);
-            after_take(L);
+            if (L + 1 < NL) issue(L + 1);
+            if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         } else {
 #pragma unroll
             for (int k = 0; k < 32; ++k) y[k] = 0u;
@@ -540,7 +451,6 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
-        line_end(L);
     }
     tile_finish<H, kMode>(a, st, r);
 }
@@ -548,44 +458,35 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 template <class H, int kMode>
 __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nwaves) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kTileWaves][8192];
-    // Wave index as a scalar: the slab base (every DMA's M0) stays in SGPRs.
-    const uint32_t lane = threadIdx.x & 63, wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    TileQueue q;
-    q.norder = a.tile_next[kTileHeads * kTileHeadStride];   // entries of `order` (pads included), from the bucketing
-    q.ntiles = (q.norder + 63) / 64;
-    q.nwaves = nwaves;
-    q.head = blockIdx.x & (kTileHeads - 1);
-    uint8_t* my_slab = &slab[wv][0];
-    TileGatherStream ls;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
+    const uint64_t ntiles = (norder + 63) / 64;
     TileClaim cl;
-    TileGeom g, gn;
     cl.t = (uint64_t)blockIdx.x * kTileWaves + wv;   // first tile: static
     cl.stage = 3;
-    if (cl.t < q.ntiles) {
-        tile_rec_load(a, tile_entry(a, cl.t, lane, q.norder), cl.r);
-        uint32_t lastc0 = 0;
-        tile_prep_geom<kMode>(a, cl, q, lane, my_slab, ls, gn, lastc0);
-        tile_prep_issue(ls, gn, lastc0);
-    }
-    while (cl.t < q.ntiles) {
+    if (cl.t < ntiles) tile_rec_load(a, tile_entry(a, cl.t, lane, norder), cl.r);
+    while (cl.t < ntiles) {
         const TileRec r = cl.r;
-        g = gn;
         cl.stage = 0;
         // The lane id re-defined per tile: what the tile derives from it
         // (bpermute addresses, slab slots, chunk numbers) is formed per tile
         // instead of being hoisted out of the loop into VGPRs held all along.
-        uint32_t ln = lane;
-        asm volatile("" : "+v"(ln));
-        if (g.stream) {
-            md_tile_stream<H, kMode>(a, r, g, ln, my_slab, ls, cl, q, gn);
+        uint32_t lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        // The tile's phase: Q (uniform) or a mixed tile.
+        // Q: 16 for a record on the second half of a 128-B line, 0 on its
+        // first half (both: the stream is whole cache lines), else the
+        // start's dword inside its 16-B chunk.
+        const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
+        const bool wl = (p32 & 63u) == 0;
+        const uint32_t Ql = wl ? ((p32 & 64u) ? 16u : 0u) : ((p32 >> 2) & 3u);
+        const uint32_t Q = (uint32_t)__builtin_amdgcn_readfirstlane(Ql);
+        if (__all(Ql == Q)) {
+            md_tile_stream<H, kMode>(a, r, lane, &slab[wv][0], Q, __all(wl), cl, ntiles, norder, nwaves);
         } else {
-            // Records that do not share a phase (small unpadded batches): the
-            // per-lane loop, with the next tile's line 0 already out.
-            uint32_t lastc_n = 0;
-            tile_prep_geom<kMode>(a, cl, q, ln, my_slab, ls, gn, lastc_n);
-            tile_prep_issue(ls, gn, lastc_n);
             md_tile_direct<H, kMode>(a, r);
         }
+        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
     }
 }
 
