@@ -56,11 +56,10 @@ struct KeyBlock {
 };
 
 // Bucket keys of ragged-batch bucketing (see lcb_kernels.hip): a length
-// class (< 122) times 6 start phases: 0 / 1 = a 16-B aligned record starting
-// in the first / second half of a 128-B line, 2 + q = a record at 4-B phase q
-// of a 16-B chunk with any byte offset beyond it (q = (start >> 2) & 3).
+// class (< 122) times 4 start phases: the start's dword inside its 16-B chunk,
+// (start >> 2) & 3 (the tile kernel's uniform block-window shift).
 constexpr int kBucketClasses = 122;
-constexpr int kBucketPhases = 6;
+constexpr int kBucketPhases = 4;
 constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
 // Bucketing scratch ahead of the permutation: key histogram, per-key fill
 // counters, the tile-queue head, the number of 64-entry tiles (uint32 words).

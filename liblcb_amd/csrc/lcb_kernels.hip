@@ -110,11 +110,10 @@ void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s) {
 // own index):
 //   class(len) = nb for nb = len/64 + 1 < 64, else 58 + floor(log2(nb))
 //   (exact block counts up to 4 KiB, power-of-two bins above), and
-//   phase     = 0 / 1 for a 16-B aligned start in the first / second half of
-//               a 128-B line (the tile kernel streams those tiles as whole
-//               cache lines), else 2 + ((start >> 2) & 3): the 4-B phase q
-//               inside the record's first 16-B chunk, which the tile
-//               kernel's byte-shifting line stream needs uniform per wave.
+//   phase     = (start >> 2) & 3: the start's dword inside its 16-B chunk,
+//               which the tile kernel's block window needs uniform per wave
+//               (the rest of the start's offset inside its 128-B line is
+//               applied per lane: md_tiles.hpp).
 // Tiles of 64 consecutive `order` entries then share their key.  For a large
 // batch every key's run is padded to whole tiles with kOrderPad entries.
 __device__ __forceinline__ uint32_t len_class(uint64_t len) {
@@ -126,8 +125,7 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
 __device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
     const uint64_t off = a.offsets ? gptr(a.offsets)[i] : i * a.stride;
     const uint32_t p = (uint32_t)(reinterpret_cast<uintptr_t>(a.data) + off);
-    const uint32_t ph = (p & 15u) == 0 ? ((p >> 6) & 1u) : 2u + ((p >> 2) & 3u);
-    return len_class(gptr(a.lengths)[i]) * kBucketPhases + ph;
+    return len_class(gptr(a.lengths)[i]) * kBucketPhases + ((p >> 2) & 3u);
 }
 
 // Few, large blocks (kBucketBlocks x 1024 threads): every block adds its LDS

@@ -11,28 +11,32 @@
 // queue head; every wave leaves once the queue is past the last tile, so the
 // grid drains.
 //
-// THE PHASE STREAM.  The records of a tile share their length class (their
-// 64-B block counts differ by at most one) and their start phase, so one
-// wave moves them through its slab by coalesced LDS-DMA as in the
-// fixed-stride kernel (GatherLineStream: 8 records x one 128-B line per
-// global_load_lds_dwordx4), from a 16-B aligned stream base, and shifts the
-// bytes into blocks in registers:
-//   phase 0 / 1 (16-B aligned record, first / second half of a 128-B line):
-//     the stream is the record's whole 128-B cache lines (base = start
-//     rounded down to 128 B), read once with the nt policy; block b is dword
-//     Q + 16 b of the stream, Q = 0 / 16;
-//   phase 2 + q (any other start): base = start rounded down to 16 B, Q = q
-//     = the start's dword inside its 16-B chunk (uniform in the tile), and
-//     the lane's own byte offset sh = start & 3 is one v_alignbyte per word
-//     (default cache policy: a 128-B stream line spans two cache lines, the
-//     second is still in L2 when the next line asks for it).
-// Block 2L is entirely in line L; block 2L - 1 needs the last 16 dwords of
-// line L - 1 (kept in VGPRs, `carry`) and dwords 0..Q of line L.  The stream
-// carries every byte of the record, the last partial line included: a DMA
-// chunk is issued only if it holds at least one byte of its record (a 16-B
-// aligned chunk never crosses a page), so no per-lane global load remains
-// and the tail, the 0x80 / length padding and the key bytes of a
-// secret-suffix message are assembled in registers from the streamed words.
+// THE WHOLE-LINE STREAM.  The records of a tile share their length class
+// (their 64-B block counts differ by at most one) and the dword phase
+// R = (start >> 2) & 3 of their start inside its 16-B chunk, so one wave
+// moves them through its slab by coalesced LDS-DMA as in the fixed-stride
+// kernel (8 records x one 128-B line per global_load_lds_dwordx4).  Every
+// record streams its own whole 128-B cache lines (base = start rounded down
+// to 128 B, nt policy: each cache line is read once), whatever its start:
+// with off = start & 127 = 64 h + 16 m + 4 R + sh,
+//   * m (the start's chunk inside its 64-B half) is applied by the DMA: the
+//     lane that fills slot k of the record's slab row loads the record's
+//     chunk (k + m) & 7, so a lane's take() of line L reads the line rotated
+//     by m chunks -- the words of the record's 16-B-aligned stream, the
+//     chunks that wrapped round being the start of line L + 1's part;
+//   * R is the tile's (uniform) dword shift of the 16-word block window and
+//     sh the lane's byte shift, one v_alignbyte per word;
+//   * h (the start's half of its line) offsets the lane's block numbering:
+//     line L completes blocks 2L - 1 - h (from the carry, the last 16 words
+//     of line L - 1, merged with line L's wrapped chunks) and 2L - h.
+// No streamed line straddles two cache lines (a 16-B aligned stream base
+// made every 128-B line two cache-line requests: 17 % of the packet stream,
+// profiles/r3_tile_diag_ab.txt), and the bucketing key needs only the 4
+// dword phases.  The stream carries every byte of the record, the last
+// partial line included: a chunk is fetched only if its cache line holds a
+// byte of its record (the line, and so its page, is the record's), so no
+// per-lane global load remains and the tail, the 0x80 / length padding and
+// the key bytes of a secret-suffix message are assembled in registers.
 //
 // Tiles that mix phases (small unpadded batches only) take the per-lane
 // message loop (md_tile_direct).
@@ -125,35 +129,42 @@ struct TileMsg {
     uint32_t kl;
 };
 
-// One block from the stream window X = c[0..15] ++ y[0..15] (c: dwords
-// 16..31 of line L - 1, y: dwords 0..15 of line L, for block 2L - 1; c = y =
-// line L for block 2L): X[Q + k] byte-shifted by sh, k = 0..15, i.e. the 16
-// raw LE words of the block (Q = 16: X[16..31] as they are).
-template <int Q>
+// One block from the stream window X = c[0..15] ++ y[0..15] (c: the carry
+// merged with line L's wrapped chunks, y: line L, for the carry block; c = y
+// = line L for the line's own block): X[R + k] byte-shifted by sh, k = 0..15,
+// i.e. the 16 raw LE words of the block.
+template <int R>
 __device__ __forceinline__ void tile_shift(const uint32_t* c, const uint32_t* y, uint32_t sh, uint32_t w[16]) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int j = Q + k;
-        if (Q == 16) {
-            w[k] = y[k];
-        } else {
-            const uint32_t lo = j < 16 ? c[j] : y[j - 16];
-            const uint32_t hi = j + 1 < 16 ? c[j + 1] : y[j + 1 - 16];
-            w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        }
+        const int j = R + k;
+        const uint32_t lo = j < 16 ? c[j] : y[j - 16];
+        const uint32_t hi = j + 1 < 16 ? c[j + 1] : y[j + 1 - 16];
+        w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
 }
-// Dispatch on the tile's (wave-uniform) Q.  Q passes through an empty asm at
-// every call so the compiler does not clone the whole line loop per Q.
-__device__ __forceinline__ void tile_assemble(uint32_t Q, const uint32_t* c, const uint32_t* y, uint32_t sh,
+// Dispatch on the tile's (wave-uniform) R.  R passes through an empty asm at
+// every call so the compiler does not clone the whole line loop per R.
+__device__ __forceinline__ void tile_assemble(uint32_t R, const uint32_t* c, const uint32_t* y, uint32_t sh,
                                               uint32_t w[16]) {
-    asm volatile("" : "+s"(Q));
-    switch (Q) {
+    asm volatile("" : "+s"(R));
+    switch (R) {
     case 0: tile_shift<0>(c, y, sh, w); break;
     case 1: tile_shift<1>(c, y, sh, w); break;
     case 2: tile_shift<2>(c, y, sh, w); break;
-    case 3: tile_shift<3>(c, y, sh, w); break;
-    default: tile_shift<16>(c, y, sh, w); break;
+    default: tile_shift<3>(c, y, sh, w); break;
+    }
+}
+
+// The carry block's first 16 words: word j of the lane's rotated stream is
+// still the carry (dwords 16..31 of line L - 1) while its chunk j >> 2 + m
+// lies below 4, else it wrapped round into line L (y[16 + j]).
+__device__ __forceinline__ void tile_merge(uint32_t* c, const uint32_t* y, uint32_t m) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool keep = (uint32_t)q + m < 4u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[4 * q + i] = keep ? c[4 * q + i] : y[16 + 4 * q + i];
     }
 }
 
@@ -169,15 +180,16 @@ __device__ __forceinline__ void tile_compress(H& st, const uint32_t* w) {
 // message blocks go straight to compress; the block holding the message's
 // end gets its bytes past the end cleared, the 0x80 terminator and, in the last block, the bit length of
 // prefix + total (md5.h:266-288).  Lanes whose message has fewer blocks do
-// nothing.  nfull_min: wave minimum of whole message blocks (uniform fast path).
+// nothing (b = 2^32 - 1: a lane whose first block starts in the next line).
+// whole: every lane's block b is a whole message block (uniform fast path).
 template <class H, int kMode>
 __device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint64_t len, const TileMsg<H, kMode>& m,
-                                           uint32_t nblk, uint32_t nfull_min) {
-    if (b < nfull_min) {           // wave-uniform: every lane has a whole message block here
+                                           uint32_t nblk, bool whole) {
+    if (whole) {                   // wave-uniform: every lane has a whole message block here
         tile_compress(st, w);
         return;
     }
-    if (b >= nblk) return;         // this lane is done
+    if (b >= nblk) return;         // this lane is done (or has no block here: b = -1)
     const uint64_t pos = (uint64_t)b * 64;
     if (pos + 64 > len) {          // the block holds the end of the message
         const int rb = pos >= len ? 0 : (int)(len - pos);   // message bytes in the block
@@ -256,36 +268,46 @@ __device__ __forceinline__ void md_tile_direct(const KArgs& a, const TileRec& r)
 
 // The tile's line stream: line L of the 64 records moves into the wave's
 // 8 KiB slab with 8 global_load_lds_dwordx4.  Lane group q (lanes 8q ..
-// 8q + 7) carries, in instruction g, the whole 128-B line of record 8q + g
-// (one of its own lanes' records), lane 8q + c its chunk c ^ g: the texture
-// unit sees 8 whole lines per instruction, not 64 partial ones, and what a
-// DMA lane needs of the record it moves comes from inside its 8-lane group.
-// Instruction g lands at slab row 8g + q, so record j's line is row
-// R(j) = 8 (j & 7) + (j >> 3), its chunk k in slot k ^ (j & 7): the 16 lanes
-// of a ds_read_b128 group hit 16 different bank groups.
-// Addressing: the saddr form, a wave-uniform scalar base (the tile's lowest
-// stream base + 128 L) plus one 32-bit offset per instruction (8 VGPRs;
-// md_tile_stream checks that the tile spans less than 4 GiB).  In the last
-// lines (masked) a chunk that holds no byte of its record is fetched from
-// the record's first chunk instead: same page, the data never used.  Which
-// chunks are valid comes from one word per group per line: every lane's
-// count of valid chunks in the line, 4 bits each, OR-reduced in the group.
+// 8q + 7) carries, in instruction g, the whole 128-B cache line L of record
+// j = 8q + g (one of its own lanes' records), lane 8q + c the record's chunk
+// (c ^ g) + m_j (mod 8; m_j: record j's chunk rotation): the texture unit
+// sees 8 whole cache lines per instruction.  Instruction g lands at slab row
+// 8g + q, so record j's line is row R(j) = 8 (j & 7) + (j >> 3), its rotated
+// chunk k in slot k ^ (j & 7): the 16 lanes of a ds_read_b128 group hit 16
+// different bank groups.  Addressing: the saddr form, a wave-uniform scalar
+// base (the tile's lowest stream base + 128 L) plus one 32-bit offset per
+// instruction (8 VGPRs; md_tile_stream checks that the tile spans less than
+// 4 GiB).  In the last lines (masked) a chunk past its record's last byte is
+// fetched from the record's first chunk instead (the data never used).
+// Which chunks are valid comes from one word per group per line: every
+// lane's count of valid chunks in the line, 4 bits each, OR-reduced in the
+// group; the group's rotations travel the same way, 2 bits each, once.
 struct TileGatherStream {
     uint8_t* slab;
     uint32_t lane;
     const uint8_t* tb;      // wave-uniform: the tile's lowest stream base
     uint32_t voff[8];       // instruction g: this lane's chunk of record 8 (lane >> 3) + g, bytes from tb
-    __device__ __forceinline__ void init(const uint8_t* tile_base, uint32_t rel, uint32_t ln, uint8_t* my_slab) {
+    // The rotations of the lane's group of 8 records, 2 bits each.
+    __device__ __forceinline__ static uint32_t group_rot(uint32_t m, uint32_t ln) {
+        uint32_t mpk = m << (2u * (ln & 7u));
+        mpk |= (uint32_t)__shfl_xor((int)mpk, 1, 64);
+        mpk |= (uint32_t)__shfl_xor((int)mpk, 2, 64);
+        mpk |= (uint32_t)__shfl_xor((int)mpk, 4, 64);
+        return mpk;
+    }
+    __device__ __forceinline__ void init(const uint8_t* tile_base, uint32_t rel, uint32_t m, uint32_t ln,
+                                         uint8_t* my_slab) {
         lane = ln;
         slab = my_slab;
         tb = tile_base;
+        const uint32_t mpk = group_rot(m, ln);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             const uint32_t rj = (uint32_t)__shfl((int)rel, (int)(ln & ~7u) + g, 64);
-            voff[g] = rj + ((ln & 7u) ^ (uint32_t)g) * 16u;
+            const uint32_t mj = (mpk >> (2 * g)) & 3u;
+            voff[g] = rj + ((((ln & 7u) ^ (uint32_t)g) + mj) & 7u) * 16u;
         }
     }
-    template <int kAux>
     __device__ __forceinline__ void issue(uint32_t L) {
         asm volatile("" : "+v"(voff[0]), "+v"(voff[1]), "+v"(voff[2]), "+v"(voff[3]), "+v"(voff[4]),
                      "+v"(voff[5]), "+v"(voff[6]), "+v"(voff[7]));
@@ -295,11 +317,12 @@ struct TileGatherStream {
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g]),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             kLdsAux);
     }
-    // lastc: index of this lane's last stream chunk holding a record byte.
-    template <int kAux>
-    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc) {
+    // lastc: index of this lane's last stream chunk holding a record byte;
+    // m: its record's rotation.
+    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc, uint32_t m) {
         // The lane id re-defined per call: the per-lane chunk numbers below
         // are not hoisted out of the tile loop (16 VGPRs held all along).
         uint32_t ln = lane;
@@ -310,16 +333,18 @@ struct TileGatherStream {
         nv |= (uint32_t)__shfl_xor((int)nv, 1, 64);
         nv |= (uint32_t)__shfl_xor((int)nv, 2, 64);
         nv |= (uint32_t)__shfl_xor((int)nv, 4, 64);
+        const uint32_t mpk = group_rot(m, ln);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint32_t k = (ln & 7u) ^ (uint32_t)g;
+            const uint32_t k = (((ln & 7u) ^ (uint32_t)g) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
             const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0, kAux);
+                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             kLdsAux);
         }
     }
-    // Waits for the issued line, copies this lane's 128 B (raw LE words); the
-    // slab is free again on return.
+    // Waits for the issued line, copies this lane's 128 B (raw LE words, the
+    // record's chunks rotated by its m); the slab is free again on return.
     __device__ __forceinline__ void take(uint32_t y[32]) const {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -338,35 +363,46 @@ struct TileGatherStream {
 
 template <class H, int kMode>
 __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
-                                               uint32_t Q, bool whole_lines, TileClaim& cl, uint64_t ntiles,
-                                               uint32_t norder, uint32_t nwaves) {
+                                               uint32_t R, TileClaim& cl, uint64_t ntiles, uint32_t norder,
+                                               uint32_t nwaves) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
     const uint32_t sh = p32 & 3u;
-    // Stream offset of the record's first byte: base = p - off0.
-    const uint32_t off0 = Q == 16 ? 64u : (p32 & 15u);
+    const uint32_t off = p32 & 127u;              // stream offset of the record's first byte
+    const uint32_t h = off >> 6, m = (off >> 4) & 3u;
+    // h and m re-derived from the start at each use (one v_bfe), not held in
+    // VGPRs through the line loop.
+    auto rot = [&]() { uint32_t v = p32; asm volatile("" : "+v"(v)); return (v >> 4) & 3u; };
+    auto half = [&]() { uint32_t v = p32; asm volatile("" : "+v"(v)); return (v >> 6) & 1u; };
     const uint64_t len = r.len;
     H st;
-    TileMsg<H, kMode> m;
-    tile_state(a, r, st, m);
-    // Geometry: lines holding record bytes, lines wholly inside every record,
-    // blocks of the padded (virtual) message, whole message blocks.
-    const uint64_t end = off0 + len;                        // record end, in stream bytes
-    const uint32_t nblk = (uint32_t)((m.total + 8u) >> 6) + 1u;
-    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7), NB = nblk, NF = r.len >> 6;
+    TileMsg<H, kMode> m_;
+    tile_state(a, r, st, m_);
+    // Geometry: lines holding record bytes (max, and min of lines wholly
+    // inside the record), blocks of the padded (virtual) message + h (max),
+    // lines whose two blocks are whole message blocks (min), whole message
+    // blocks (min).
+    const uint64_t end = off + len;                          // record end, in stream bytes
+    const uint32_t nblk = (uint32_t)((m_.total + 8u) >> 6) + 1u;
+    const uint32_t nf = r.len >> 6;
+    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7), NB = nblk + h;
+    uint32_t LF = (nf + h + 1u) >> 1, NF = nf;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {                       // wave max / min (xor butterfly)
         NL = max(NL, (uint32_t)__shfl_xor((int)NL, d, 64));
         NB = max(NB, (uint32_t)__shfl_xor((int)NB, d, 64));
         NS = min(NS, (uint32_t)__shfl_xor((int)NS, d, 64));
+        LF = min(LF, (uint32_t)__shfl_xor((int)LF, d, 64));
         NF = min(NF, (uint32_t)__shfl_xor((int)NF, d, 64));
     }
     NL = __builtin_amdgcn_readfirstlane(NL);
     NB = __builtin_amdgcn_readfirstlane(NB);
     NS = __builtin_amdgcn_readfirstlane(NS);
+    LF = __builtin_amdgcn_readfirstlane(LF);
     NF = __builtin_amdgcn_readfirstlane(NF);
+    if (LF > NL) LF = NL;
     // The tile's stream bases: 32-bit offsets from the lowest (saddr form)
     // when the tile spans less than 4 GiB, else the per-lane loop.
-    const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off0;
+    const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off;
     uint64_t lo = base, hi = base;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -375,35 +411,32 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     }
     lo = readfirstlane64(lo);
     hi = readfirstlane64(hi);
-    if (hi - lo + (uint64_t)(NL + 1) * 128u >= (1ull << 32) || !__all(end != 0)) {
-        if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m.K, m.kl, 0);
-        else md_message(st, r.p, r.len, m.prefix);
+    if (hi - lo + (uint64_t)(NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
+        if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m_.K, m_.kl, 0);
+        else md_message(st, r.p, r.len, m_.prefix);
         tile_finish<H, kMode>(a, st, r);
         return;
     }
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
+    // No lane's chunks rotated (every start on a 64-B half line, as in C4):
+    // the carry needs no merge (wave-uniform).
+    const bool rotated = !__all(m == 0);
     TileGatherStream ls;
-    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(base - lo), lane, slab);
+    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(base - lo), m, lane, slab);
     auto issue = [&](uint32_t L) {
-        if (L >= NS) {
-            if (whole_lines) ls.issue_masked<kLdsAux>(L, lastc);
-            else ls.issue_masked<kGatherAux>(L, lastc);
-        } else {
-            if (whole_lines) ls.issue<kLdsAux>(L);
-            else ls.issue<kGatherAux>(L);
-        }
+        if (L >= NS) ls.issue_masked(L, lastc, rot());
+        else ls.issue(L);
     };
     const uint32_t c0 = NL > 3 ? NL - 3 : 0u;                // first claim step
-    if (NL) issue(0);
-    uint32_t c[16];   // dwords 16..31 of the previous line (the carry)
-    // Whole-block lines: both blocks of line L (2L - 1 and 2L) are whole
-    // message blocks of every lane (2L < NF).
-    const uint32_t LF = (NF + 1) / 2 < NL ? (NF + 1) / 2 : NL;
     // Keyed suffix: the stream ends with the whole-block lines, the rest
     // (under two lines of message, the key) goes through the per-lane loop:
     // the key's window assembly next to a streamed line needs more VGPRs
     // than the occupancy leaves.
     const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
+    if (LE) issue(0);
+    uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
+    // Whole-block lines: both blocks of line L (2L - 1 - h and 2L - h) are
+    // whole message blocks of every lane.
     uint32_t L = 0;
     for (; L < LF; ++L) {
         uint32_t y[32];
@@ -411,26 +444,28 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         if (L + 1 < LE) issue(L + 1);
         if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         uint32_t w[16];
-        if (L > 0) {   // block 2L - 1: the carry and dwords 0..Q of this line
-            tile_assemble(Q, c, y, sh, w);
+        if (L > 0) {   // block 2L - 1 - h: the carry merged with this line's wrapped chunks
+            if (rotated) tile_merge(c, y, rot());
+            tile_assemble(R, c, y, sh, w);
             tile_compress(st, w);
         }
-        tile_assemble(Q, y, y + 16, sh, w);   // block 2L: dwords Q..Q+16 of this line
-        tile_compress(st, w);
+        tile_assemble(R, y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
+        if (L > 0 || half() == 0) tile_compress(st, w);
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
     }
     if constexpr (kMode == kTileKeyedSuffix) {
-        const uint64_t done = LF ? (2ull * LF - 1) * 64u : 0u;   // blocks 0 .. 2 LF - 2
+        const uint32_t nd = LF ? 2u * LF - 1u - half() : 0u;       // blocks 0 .. nd - 1 done
+        const uint64_t done = (uint64_t)nd * 64u;
         while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
-        md_message2(st, r.p + done, len - done, m.K, m.kl, m.prefix + done);
+        md_message2(st, r.p + done, len - done, m_.K, m_.kl, m_.prefix + done);
         tile_finish<H, kMode>(a, st, r);
         return;
     }
     // The rest, line by line (tile_block: ends of messages, padding, length);
     // lines past the last streamed one are zeros (those bytes lie past every
     // record's end).
-    for (; 2 * L <= NB; ++L) {   // block 2L - 1 < NB
+    for (; 2 * L <= NB; ++L) {   // block 2L - 1 - h < nblk for some lane
         uint32_t y[32];
         if (L < NL) {
             ls.take(y);
@@ -442,12 +477,13 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         }
         uint32_t w[16];
         if (L > 0) {
-            tile_assemble(Q, c, y, sh, w);
-            tile_block<H, kMode>(st, 2 * L - 1, w, len, m, nblk, NF);
+            if (rotated) tile_merge(c, y, rot());
+            tile_assemble(R, c, y, sh, w);
+            tile_block<H, kMode>(st, 2 * L - 1 - half(), w, len, m_, nblk, 2 * L - 1 < NF);
         }
         if (2 * L < NB) {
-            tile_assemble(Q, y, y + 16, sh, w);
-            tile_block<H, kMode>(st, 2 * L, w, len, m, nblk, NF);
+            tile_assemble(R, y, y + 16, sh, w);
+            tile_block<H, kMode>(st, 2 * L - half(), w, len, m_, nblk, 2 * L < NF && L > 0);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
@@ -473,16 +509,11 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
         // instead of being hoisted out of the loop into VGPRs held all along.
         uint32_t lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
-        // The tile's phase: Q (uniform) or a mixed tile.
-        // Q: 16 for a record on the second half of a 128-B line, 0 on its
-        // first half (both: the stream is whole cache lines), else the
-        // start's dword inside its 16-B chunk.
-        const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
-        const bool wl = (p32 & 63u) == 0;
-        const uint32_t Ql = wl ? ((p32 & 64u) ? 16u : 0u) : ((p32 >> 2) & 3u);
-        const uint32_t Q = (uint32_t)__builtin_amdgcn_readfirstlane(Ql);
-        if (__all(Ql == Q)) {
-            md_tile_stream<H, kMode>(a, r, lane, &slab[wv][0], Q, __all(wl), cl, ntiles, norder, nwaves);
+        // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
+        const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
+        if (__all(Rl == R)) {
+            md_tile_stream<H, kMode>(a, r, lane, &slab[wv][0], R, cl, ntiles, norder, nwaves);
         } else {
             md_tile_direct<H, kMode>(a, r);
         }

@@ -411,3 +411,46 @@ def test_c4_full_size(gpu, large):
         assert dod(d) == fx["algs"][name]["dod"], name
     del data
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", ["short", "lines"])
+def test_ragged_every_line_phase(gpu, oracle, shape):
+    """The tile kernel's whole-cache-line stream (md_tiles.hpp): records start
+    at every one of the 128 byte offsets inside a 128-B line (off = 64 h + 16 m
+    + 4 R + sh: the tile's dword phase R from the bucketing, the lane's chunk
+    rotation m applied by the DMA addresses and merged into the carry, its
+    half-line h offsetting its block numbering, its byte shift sh), so every
+    tile of a key mixes all (h, m, sh).  Lengths 1..700 ("short": records of
+    1-6 lines, tails of every size) or whole lines +- a few bytes ("lines"),
+    a few 4 KiB records, the last record ending at the buffer's end.  MD5
+    plain, HMAC, keyed HMAC and keyed suffix (the tile kernel's modes) digest
+    by digest against the oracle."""
+    rng = np.random.default_rng({"short": 11, "lines": 12}[shape])
+    n = 8192
+    if shape == "short":
+        lens = rng.integers(1, 701, n)
+    else:
+        lens = 128 * rng.integers(1, 12, n) + rng.integers(-3, 4, n)
+    lens[rng.integers(0, n, 50)] = 4096
+    lens = lens.astype(np.uint32)
+    phase = rng.permutation(np.arange(n) % 128)
+    offs = np.zeros(n, np.uint64)
+    pos = 0
+    for k in range(n):
+        pos = pos + (int(phase[k]) - pos) % 128
+        offs[k] = pos
+        pos += int(lens[k])
+    data = gen_stream(17, pos)
+    dd, dl, do = dev(data), dev(lens, np.int32), dev(offs, np.int64)
+    exp = oracle.batch(1, data, offs, lens)
+    assert np.array_equal(gpu.hash_batch(1, dd, offsets=do, lengths=dl).cpu().numpy(), exp), shape
+    exp = oracle.batch(1, data, offs, lens, key=b"radius-secret")
+    got = gpu.hash_batch(1, dd, offsets=do, lengths=dl, key=b"radius-secret").cpu().numpy()
+    assert np.array_equal(got, exp), shape
+    keys = [bytes(range(7 + 13 * k)) for k in range(5)]
+    kidx = rng.integers(0, len(keys), n).astype(np.uint32)
+    for mode in (1, 3):   # LCB_HASH_KEY_HMAC, LCB_HASH_KEY_SUFFIX
+        exp = oracle.batch_keyed(1, mode, keys, data, kidx, offs, lens)
+        got = gpu.hash_batch_keyed(1, mode, keys, dd, key_index=dev(kidx, np.int32), offsets=do,
+                                   lengths=dl).cpu().numpy()
+        assert np.array_equal(got, exp), (shape, mode)
