@@ -62,6 +62,10 @@ inline uint64_t st_count(uint64_t s) { return (s >> kCountShift) & kCountMask; }
 // h_off entry of a zero-copy packet: this bit | its device address (user
 // addresses are far below 2^63); arena packets hold their arena position.
 constexpr uint64_t kZeroCopyTag = 1ull << 63;
+// Zero-copy runs per batch moved by bulk H2D copies, and the largest gap
+// between two packets of one run (bytes copied but never hashed).
+constexpr int kZcRuns = 32;
+constexpr uint64_t kZcGap = 256;
 inline uint64_t st_bytes(uint64_t s) { return s & kBytesMask; }
 
 struct Meta {
@@ -94,6 +98,7 @@ struct Slot {
     uint32_t* h_len = nullptr;
     uint8_t* h_dig = nullptr;
     Meta* meta = nullptr;
+    uint8_t* zrun = nullptr;                     // launch: run of each zero-copy packet (kZcRuns = none)
     LeaseRec* leases = nullptr;
     size_t nleases = 0;
     uint8_t* d_data = nullptr;
@@ -267,12 +272,61 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
     // Offsets become absolute device addresses (the batch's `data` is 0):
     // arena packets at d_data + pos, zero-copy packets where they lie in
     // host memory (kZeroCopyTag | device address, from the submit).
+    // Zero-copy packets: every producer submits from its own receive buffers
+    // in address order, so a batch's zero-copy packets form a few contiguous
+    // RUNS (one per producer stream; gaps up to kZcGap bytes are bridged).
+    // Runs that lie in one registered region and fit the slot's device arena
+    // beside the copied packets move with one H2D copy each, at the link's
+    // bulk rate, and are hashed from device memory; a packet outside them is
+    // read by the kernel where it lies, over the link.
     const uint64_t arena = (uint64_t)reinterpret_cast<uintptr_t>(b->d_data);
+    struct Run { uint64_t lo, hi; };
+    Run run[kZcRuns];
+    int nrun = 0, last = -1;
+    // The arena bytes the copied packets fill (leases reserve room that a
+    // lease's zero-copy packets, or its unused tail, never write).
+    uint64_t aused = 0;
+    for (size_t i = 0; i < b->n; ++i) {
+        const uint64_t o = b->h_off[i];
+        b->zrun[i] = kZcRuns;
+        if (!(o & kZeroCopyTag)) {
+            aused = std::max<uint64_t>(aused, o + b->h_len[i]);
+            continue;
+        }
+        const uint64_t d = o & ~kZeroCopyTag, e = d + b->h_len[i];
+        int r = -1;
+        if (last >= 0 && d >= run[last].hi && d <= run[last].hi + kZcGap) r = last;
+        for (int k = 0; k < nrun && r < 0; ++k)
+            if (d >= run[k].hi && d <= run[k].hi + kZcGap) r = k;
+        if (r < 0 && nrun < kZcRuns) { r = nrun++; run[r].lo = d; run[r].hi = d; }
+        if (r < 0) continue;                       // too many runs: read in place
+        run[r].hi = e;
+        b->zrun[i] = (uint8_t)r;
+        last = r;
+    }
+    // Arena position of each run (after the copied packets, 256-B aligned);
+    // runs that do not fit or leave every registered region stay in place.
+    uint64_t rpos[kZcRuns];
+    const uint8_t* rhost[kZcRuns];
+    uint64_t pos = (aused + 255) & ~255ull;
+    const int nr = nregions.load(std::memory_order_acquire);
+    for (int k = 0; k < nrun; ++k) {
+        rhost[k] = nullptr;
+        const uint64_t len = run[k].hi - run[k].lo;
+        if (pos + len > cfg.max_batch_bytes) continue;
+        for (int g = 0; g < nr && !rhost[k]; ++g)
+            if (run[k].lo >= regions[g].dev && run[k].hi <= regions[g].dev + regions[g].size)
+                rhost[k] = regions[g].host + (run[k].lo - regions[g].dev);
+        if (rhost[k]) { rpos[k] = pos; pos = (pos + len + 255) & ~255ull; }
+    }
     for (size_t i = 0; i < b->n; ++i) {
         payload += b->h_len[i];
         packets += b->meta[i].real;
         const uint64_t o = b->h_off[i];
-        b->h_off[i] = (o & kZeroCopyTag) ? (o & ~kZeroCopyTag) : arena + o;
+        const int r = b->zrun[i];
+        if (!(o & kZeroCopyTag)) b->h_off[i] = arena + o;
+        else if (r < kZcRuns && rhost[r]) b->h_off[i] = arena + rpos[r] + ((o & ~kZeroCopyTag) - run[r].lo);
+        else b->h_off[i] = o & ~kZeroCopyTag;
     }
     b->payload = payload;
     b->packets = packets;
@@ -283,8 +337,12 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
     int rc = 0;
     if (hipMemcpyAsync(b->d_off, b->h_off, b->n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b->d_len, b->h_len, b->n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-        (b->bytes && hipMemcpyAsync(b->d_data, b->h_data, b->bytes, hipMemcpyHostToDevice, st) != hipSuccess))
+        (aused && hipMemcpyAsync(b->d_data, b->h_data, aused, hipMemcpyHostToDevice, st) != hipSuccess))
         rc = EIO;
+    for (int k = 0; k < nrun && !rc; ++k)
+        if (rhost[k] && run[k].hi > run[k].lo &&
+            hipMemcpyAsync(b->d_data + rpos[k], rhost[k], run[k].hi - run[k].lo, hipMemcpyHostToDevice, st) != hipSuccess)
+            rc = EIO;
     if (!rc) rc = launch_ordered(alg, a, st, b->d_work);
     if (!rc && hipMemcpyAsync(b->h_dig, b->d_dig, b->n * D, hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = EIO;
@@ -449,6 +507,8 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), bucket_words(msgs) * sizeof(uint32_t)));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
+    b.zrun = new (std::nothrow) uint8_t[msgs];
+    if (!b.zrun) return ENOMEM;
     b.leases = new (std::nothrow) LeaseRec[nleases];
     b.nleases = nleases;
     if (!b.meta || !b.leases) return ENOMEM;
@@ -482,8 +542,9 @@ void free_slot(Slot& b) {
     if (b.done) (void)hipEventDestroy(b.done);
     if (b.stream) (void)hipStreamDestroy(b.stream);
     delete[] b.meta;
+    delete[] b.zrun;
     delete[] b.leases;
-    b.h_data = nullptr; b.h_off = nullptr; b.h_len = nullptr; b.h_dig = nullptr; b.meta = nullptr;
+    b.h_data = nullptr; b.h_off = nullptr; b.h_len = nullptr; b.h_dig = nullptr; b.meta = nullptr; b.zrun = nullptr;
     b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_dig = nullptr; b.d_work = nullptr;
     b.done = nullptr; b.stream = nullptr; b.leases = nullptr; b.nleases = 0;
 }

@@ -291,11 +291,15 @@ def test_stale_lease_across_generations(gpu, oracle):
 
 # ------------------------------------------------------------ zero copy
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["scattered", "ring"])
 @pytest.mark.parametrize("alg,key", [(MD5, None), (MD5, b"radius-shared-secret"), (SHA256, None)])
-def test_zerocopy_submit(gpu, oracle, alg, key):
+def test_zerocopy_submit(gpu, oracle, alg, key, layout):
     """LCB_HASH_Q_F_ZEROCOPY: packets at byte offsets inside a registered
-    pinned area, hashed in place (mixed with copied submits), from several
-    threads, over many batches; digests == oracle."""
+    pinned area (mixed with copied submits), from several threads, over many
+    batches; digests == oracle.  "scattered": random offsets over 8 MiB, so a
+    batch's packets are sparse in their span and the kernel reads them in
+    host memory; "ring": packets back to back as in a receive ring, so a
+    batch's span moves with one H2D copy (lcb_hash_queue.cpp launch)."""
     import torch
     from liblcb_amd.queue import HashQueue
     from liblcb_amd._lib import DIGEST_SIZE
@@ -305,9 +309,14 @@ def test_zerocopy_submit(gpu, oracle, alg, key):
     area[:] = rng.integers(0, 256, area.size, dtype=np.uint8)
     n = 6000
     lens = rng.integers(0, 1600, n)
-    offs = rng.integers(0, area.size - 1600, n)
-    lens[:4] = (0, 1, 64, 1599)
-    offs[:4] = (0, area.size - 1, area.size - 64, area.size - 1599)   # ends exactly at the area's end
+    if layout == "scattered":
+        offs = rng.integers(0, area.size - 1600, n)
+        lens[:4] = (0, 1, 64, 1599)
+        offs[:4] = (0, area.size - 1, area.size - 64, area.size - 1599)   # ends exactly at the area's end
+    else:
+        offs = np.zeros(n, np.int64)
+        offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 3, n - 1))
+        offs += area.size - int(offs[-1] + lens[-1])                      # the last ends at the area's end
     pkts = [area[o:o + l] for o, l in zip(offs, lens)]
     want = _oracle_digests(oracle, alg, [p.copy() for p in pkts], key)
     got = np.zeros((n, DIGEST_SIZE[alg]), np.uint8)
