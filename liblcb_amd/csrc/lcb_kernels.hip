@@ -203,7 +203,9 @@ __global__ __launch_bounds__(1024) void bucket_scatter_kernel(KArgs a, const uin
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allow_pad, hipStream_t s) {
     // work: histogram | fill counters | tile-queue head | tile count, zeroed
     // here; order: bucket_words(count) - kBucketWork uint32.
-    (void)hipMemsetAsync(work, 0, kBucketWork * sizeof(uint32_t), s);
+    // Rounded up to 16 B: one fill kernel instead of a body and a tail (the
+    // bytes past kBucketWork are `order` entries the scatter writes anyway).
+    (void)hipMemsetAsync(work, 0, (kBucketWork * sizeof(uint32_t) + 15) & ~(size_t)15, s);
     uint64_t nb = (a.count + 1023) / 1024;
     if (nb > kBucketBlocks) nb = kBucketBlocks;
     const uint64_t chunk = (a.count + nb - 1) / nb;

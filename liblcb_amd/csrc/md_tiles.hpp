@@ -361,10 +361,9 @@ struct TileGatherStream {
     }
 };
 
-template <class H, int kMode>
+template <class H, int kMode, int kR>
 __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
-                                               uint32_t R, TileClaim& cl, uint64_t ntiles, uint32_t norder,
-                                               uint32_t nwaves) {
+                                               TileClaim& cl, uint64_t ntiles, uint32_t norder, uint32_t nwaves) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
     const uint32_t sh = p32 & 3u;
     const uint32_t off = p32 & 127u;              // stream offset of the record's first byte
@@ -446,10 +445,10 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         uint32_t w[16];
         if (L > 0) {   // block 2L - 1 - h: the carry merged with this line's wrapped chunks
             if (rotated) tile_merge(c, y, rot());
-            tile_assemble(R, c, y, sh, w);
+            tile_shift<kR>(c, y, sh, w);
             tile_compress(st, w);
         }
-        tile_assemble(R, y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
+        tile_shift<kR>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
         if (L > 0 || half() == 0) tile_compress(st, w);
 #pragma unroll
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
@@ -478,11 +477,11 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         uint32_t w[16];
         if (L > 0) {
             if (rotated) tile_merge(c, y, rot());
-            tile_assemble(R, c, y, sh, w);
+            tile_shift<kR>(c, y, sh, w);
             tile_block<H, kMode>(st, 2 * L - 1 - half(), w, len, m_, nblk, 2 * L - 1 < NF);
         }
         if (2 * L < NB) {
-            tile_assemble(R, y, y + 16, sh, w);
+            tile_shift<kR>(y, y + 16, sh, w);
             tile_block<H, kMode>(st, 2 * L - half(), w, len, m_, nblk, 2 * L < NF && L > 0);
         }
 #pragma unroll
@@ -513,7 +512,15 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
         const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
         if (__all(Rl == R)) {
-            md_tile_stream<H, kMode>(a, r, lane, &slab[wv][0], R, cl, ntiles, norder, nwaves);
+            // One copy of the line loop per dword phase R: the block window's
+            // word selection is static (no per-call dispatch and the register
+            // moves that merge its cases).
+            switch (R) {
+            case 0: md_tile_stream<H, kMode, 0>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
+            case 1: md_tile_stream<H, kMode, 1>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
+            case 2: md_tile_stream<H, kMode, 2>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
+            default: md_tile_stream<H, kMode, 3>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
+            }
         } else {
             md_tile_direct<H, kMode>(a, r);
         }
