@@ -493,7 +493,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 template <class H, int kMode>
 __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nwaves) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kTileWaves][8192];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // Wave index as a scalar: the slab base (every DMA's M0) stays in SGPRs.
+    const uint32_t lane = threadIdx.x & 63, wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
     const uint64_t ntiles = (norder + 63) / 64;
     TileClaim cl;
