@@ -5,7 +5,7 @@
 # bytes and kernel time (kbench).  Each step has its own limit; the script
 # stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r3b}
+TAG=${TAG:-r3d}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
