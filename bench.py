@@ -423,8 +423,9 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
     mix64(seed + i) % 3, packed, device resident.  The library
     buckets the ragged batch by length on the device (counted in the time).
     One pass per algorithm of `algs` over the same bytes (the first is the
-    headline; MD5 runs the tile kernel, the others the per-lane kernel over the
-    bucketed order), each checked against the reference's digest-of-digests."""
+    headline; MD5, SHA-1 and SHA-224/256 run the tile kernel, SHA-384/512 and
+    GOST the per-lane kernel over the bucketed order), each checked against
+    the reference's digest-of-digests."""
     from tests.golden_util import mixed_lengths
     lens = np.array(mixed_lengths(SEED, count), dtype=np.uint32)
     offs = np.zeros(count, dtype=np.uint64)
@@ -806,9 +807,10 @@ def main():
         c4 = bench_c4([alg] + [ALG_IDS[n] for n in ("sha1", "sha256", "sha512", "gost256") if ALG_IDS[n] != alg],
                       a.warmup, max(3, a.steps // 4))
         out["ragged_c4"] = c4.pop(ALG_NAMES[alg])
-        # The other algorithms on C4 (per-lane kernels over the bucketed
-        # order), with their fixed-stride rate for comparison: VALU-bound, so
-        # ragged ~ fixed means the per-lane loads are hidden.
+        # The other algorithms on C4 (SHA-1/256: the tile kernel; SHA-512,
+        # GOST: per-lane kernels over the bucketed order), with their
+        # fixed-stride rate for comparison: VALU-bound, so ragged ~ fixed
+        # means the ragged machinery is hidden.
         for name, r in c4.items():
             if name in per:
                 r["fixed_stride_GiB_s"] = per[name]["GiB_s"]

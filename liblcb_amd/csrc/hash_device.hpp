@@ -352,7 +352,10 @@ struct Sha1 {
     static constexpr bool kPairLoad = true;
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
-    static constexpr int kTileOcc = 0;   // the tile kernel spills at 80 VGPRs: ragged batches go per-lane
+    // Ragged batches: the tile kernel at 2 waves per SIMD (182-192 VGPRs, no
+    // scratch; at 3 or 4 it spills): packets 2-3 % faster than per-lane, C4 equal
+    // (profiles/r3_sha_tiles_ab.txt).
+    static constexpr int kTileOcc = 2;
     uint32_t s[5];
     __device__ __forceinline__ void init() {
         s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
@@ -429,7 +432,10 @@ struct Sha256 {
     // Line stream on: 2.4 % faster than direct loads (profiles/r1_sha2_lds_ab.txt).
     static constexpr bool kLdsStream = true;
     static constexpr bool kScalarPad = true;
-    static constexpr int kTileOcc = 0;   // VALU-bound: ragged batches take the per-lane kernel
+    // Ragged batches: the tile kernel at 2 waves per SIMD (179-194 VGPRs, no
+    // scratch): C4 6 % faster than per-lane, packets 2 % slower
+    // (profiles/r3_sha_tiles_ab.txt).
+    static constexpr int kTileOcc = 2;
     uint32_t s[8];
     __device__ __forceinline__ void init() {
         if (k224) {  // sha2.h:129-132

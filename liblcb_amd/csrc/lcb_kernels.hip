@@ -246,10 +246,15 @@ void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint3
                        nkeys, bad);
 }
 
+// The hashes with a tile kernel (kTileOcc > 0): MD5, SHA-1, SHA-224/256.
+static_assert(Md5::kTileOcc > 0 && Sha1::kTileOcc > 0 && Sha256<true>::kTileOcc > 0 &&
+                  Sha256<false>::kTileOcc > 0 && Sha512<true>::kTileOcc == 0 && Sha512<false>::kTileOcc == 0,
+              "tiles_take must list exactly the hashes with a tile kernel");
+
 bool tiles_take(int alg, const KArgs& a) {
-    // MD5 (the only hash with a tile kernel, Md5::kTileOcc): plain, HMAC,
-    // keyed HMAC and keyed suffix batches (md_kernels.hpp launch_md*).
-    return alg == 1 && a.key_mode != kKeyPrefix;
+    // Their plain, HMAC, keyed HMAC and keyed suffix batches (md_kernels.hpp
+    // launch_md*) run the tile kernel: its runs are padded to whole tiles.
+    return alg >= 1 && alg <= 4 && a.key_mode != kKeyPrefix;
 }
 
 void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s) {

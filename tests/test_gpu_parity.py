@@ -413,8 +413,9 @@ def test_c4_full_size(gpu, large):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("alg", [1, 2, 3, 4], ids=["md5", "sha1", "sha224", "sha256"])
 @pytest.mark.parametrize("shape", ["short", "lines"])
-def test_ragged_every_line_phase(gpu, oracle, shape):
+def test_ragged_every_line_phase(gpu, oracle, shape, alg):
     """The tile kernel's whole-cache-line stream (md_tiles.hpp): records start
     at every one of the 128 byte offsets inside a 128-B line (off = 64 h + 16 m
     + 4 R + sh: the tile's dword phase R from the bucketing, the lane's chunk
@@ -422,9 +423,10 @@ def test_ragged_every_line_phase(gpu, oracle, shape):
     half-line h offsetting its block numbering, its byte shift sh), so every
     tile of a key mixes all (h, m, sh).  Lengths 1..700 ("short": records of
     1-6 lines, tails of every size) or whole lines +- a few bytes ("lines"),
-    a few 4 KiB records, the last record ending at the buffer's end.  MD5
-    plain, HMAC, keyed HMAC and keyed suffix (the tile kernel's modes) digest
-    by digest against the oracle."""
+    a few 4 KiB records, the last record ending at the buffer's end.  Every
+    hash with a tile kernel (MD5, SHA-1, SHA-224/256): plain, HMAC, keyed HMAC
+    and keyed suffix (the tile kernel's modes) digest by digest against the
+    oracle."""
     rng = np.random.default_rng({"short": 11, "lines": 12}[shape])
     n = 8192
     if shape == "short":
@@ -442,15 +444,15 @@ def test_ragged_every_line_phase(gpu, oracle, shape):
         pos += int(lens[k])
     data = gen_stream(17, pos)
     dd, dl, do = dev(data), dev(lens, np.int32), dev(offs, np.int64)
-    exp = oracle.batch(1, data, offs, lens)
-    assert np.array_equal(gpu.hash_batch(1, dd, offsets=do, lengths=dl).cpu().numpy(), exp), shape
-    exp = oracle.batch(1, data, offs, lens, key=b"radius-secret")
-    got = gpu.hash_batch(1, dd, offsets=do, lengths=dl, key=b"radius-secret").cpu().numpy()
+    exp = oracle.batch(alg, data, offs, lens)
+    assert np.array_equal(gpu.hash_batch(alg, dd, offsets=do, lengths=dl).cpu().numpy(), exp), shape
+    exp = oracle.batch(alg, data, offs, lens, key=b"radius-secret")
+    got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=b"radius-secret").cpu().numpy()
     assert np.array_equal(got, exp), shape
     keys = [bytes(range(7 + 13 * k)) for k in range(5)]
     kidx = rng.integers(0, len(keys), n).astype(np.uint32)
     for mode in (1, 3):   # LCB_HASH_KEY_HMAC, LCB_HASH_KEY_SUFFIX
-        exp = oracle.batch_keyed(1, mode, keys, data, kidx, offs, lens)
-        got = gpu.hash_batch_keyed(1, mode, keys, dd, key_index=dev(kidx, np.int32), offsets=do,
+        exp = oracle.batch_keyed(alg, mode, keys, data, kidx, offs, lens)
+        got = gpu.hash_batch_keyed(alg, mode, keys, dd, key_index=dev(kidx, np.int32), offsets=do,
                                    lengths=dl).cpu().numpy()
         assert np.array_equal(got, exp), (shape, mode)

@@ -4,7 +4,8 @@
 C4 pass, and 1M x 1 KiB described as a ragged batch at strides 1024 / 1040 /
 1025 (aligned, 16-B phase, unaligned).  One JSON line per measurement.
 
-usage: python3 tools/pkt_bench.py [--steps 20] [--algs md5,sha1] [--no-c4]"""
+usage: python3 tools/pkt_bench.py [--steps 20] [--algs md5,sha1] [--no-c4]
+                                 [--no-layouts] [--c4-algs sha1,sha256]"""
 import argparse
 import json
 import os
@@ -70,14 +71,20 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--algs", default="md5")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-layouts", action="store_true", help="skip the MD5 layout / 1 KiB rows")
+    ap.add_argument("--c4-algs", default="", help="C4 passes of these algorithms (full steps each)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     bench.settle()
     print(json.dumps({"ragged_packets": bench.bench_packets(10, a.steps, tuple(a.algs.split(",")))}), flush=True)
-    for kind in ("sorted", "aligned128"):
-        print(json.dumps(packets_layout(kind, a.steps)), flush=True)
-    for st in (1024, 1040, 1025):
-        print(json.dumps(ragged_1k(st, a.steps)), flush=True)
+    if not a.no_layouts:
+        for kind in ("sorted", "aligned128"):
+            print(json.dumps(packets_layout(kind, a.steps)), flush=True)
+        for st in (1024, 1040, 1025):
+            print(json.dumps(ragged_1k(st, a.steps)), flush=True)
+    for name in filter(None, a.c4_algs.split(",")):
+        alg = bench.ALG_IDS[name]
+        print(json.dumps({"c4": bench.bench_c4([alg], 3, max(3, a.steps // 4))[name], "alg": name}), flush=True)
     if not a.no_c4:
         print(json.dumps({"c4": bench.bench_c4([1], 5, a.steps)["md5"]}), flush=True)
 

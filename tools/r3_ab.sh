@@ -28,7 +28,7 @@ for l in open(sys.argv[1]):
     if "ragged_packets" in j:
         print("   packets", {k: (v["ms_per_pass"], v["hbm_frac"], v["dod_equals_reference"]) for k, v in j["ragged_packets"].items() if isinstance(v, dict)})
     elif "c4" in j:
-        print("   c4", j["c4"]["ms_per_pass"], j["c4"]["hbm_frac"], j["c4"].get("dod_equals_reference"))
+        print("   c4", j.get("alg", ""), j["c4"]["ms_per_pass"], j["c4"]["hbm_frac"], j["c4"].get("dod_equals_reference"))
     else:
         print("  ", j)
 PY
