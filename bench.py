@@ -696,10 +696,11 @@ def main():
         raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
     if a.plan:
         return plan(a, world, rank)
+    ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU
     if world > 1:
         # One rank per GPU (LOCAL_RANK); with gloo more ranks than GPUs share
-        # them round-robin (device_count() does not initialise the GPU).
-        local = local % max(1, torch.cuda.device_count())
+        # them round-robin.
+        local = local % ndev
         torch.cuda.set_device(local)
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -729,7 +730,10 @@ def main():
         "metric": "device-resident GiB/s hashed, 1M x 1 KiB buffers per GPU",
         "value": round(value, 3),
         "unit": "GiB/s",
-        "n_gpus": world,
+        # Physical devices the ranks ran on: a gloo run with more ranks than
+        # GPUs shares them round-robin, and then says so (never a scaling point).
+        "n_gpus": min(world, ndev),
+        "ranks_share_devices": world > ndev,
         "world_size": dist.get_world_size() if world > 1 else 1,
         "dist_backend": a.dist_backend if world > 1 else None,
         "shards": all_shards(rank, world, first, count),
@@ -744,7 +748,8 @@ def main():
         "config": {"workload": "%s digest of %d x %d B buffers over %d GPU(s), %s scaling"
                                % (a.alg, total, MSG_LEN, world, a.scaling),
                    "alg": a.alg, "buffers_per_gpu": count, "buffer_bytes": MSG_LEN,
-                   "total_buffers": total, "parallelism": "shard%d" % world,
+                   "total_buffers": total, "parallelism": "shard%d" % world + ("" if world <= ndev else
+                                                                             " (ranks share %d GPU(s))" % ndev),
                    "split": "lcb_hash_partition (work-balanced contiguous shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -93,12 +93,16 @@ typedef struct lcb_hash_queue_stats_s {
 /* Zero copy: the packet lies in a page-locked region registered with
  * lcb_hash_queue_register() (e.g. the thread pool's receive io_bufs,
  * include/utils/io_buf.h:40-47, recvfrom()'d in place,
- * src/threadpool/threadpool_task.c:692-721): the queue records its address
- * and length instead of copying its bytes, and the kernel reads it from host
- * memory over PCIe.  The bytes must stay unchanged until the packet's
- * completion (digest written / callback called).  One segment only
- * (lcb_hash_queue_submitv with nsegs == 1); EINVAL if [data, data + size) is
- * not inside one registered region. */
+ * src/threadpool/threadpool_task.c:692-721): the producer copies nothing,
+ * the queue records the packet's address and length.  When the batch
+ * launches, its zero-copy packets are coalesced into runs (a packet that
+ * follows the end of a run within 256 B extends it); every run that lies in
+ * one registered region and fits the slot's device arena moves to the device
+ * with ONE bulk host-to-device copy, and only a packet outside such a run is
+ * read by the kernel in place over PCIe.  The bytes must stay unchanged until
+ * the packet's completion (digest written / callback called).  One segment
+ * only (lcb_hash_queue_submitv with nsegs == 1); EINVAL if
+ * [data, data + size) is not inside one registered region. */
 #define LCB_HASH_Q_F_ZEROCOPY	0x0002u
 
 /* Defaults: 65536 packets, 16 MiB, 200 us, 4 slots, 16-byte alignment. */
@@ -120,7 +124,11 @@ int	lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t *segs,
 /* Register page-locked host memory (hipHostMalloc / hipHostRegister) as a
  * zero-copy packet source, for the queue's lifetime; up to 16 regions.
  * EINVAL if [base, base + size) is not page-locked memory of one allocation,
- * ENOMEM when the table is full.  Call before the submits that use it. */
+ * ENOMEM when the table is full.  Call before the submits that use it.
+ * There is no unregister: a registered region must stay allocated and
+ * page-locked until lcb_hash_queue_destroy() has returned (submits validate
+ * against the table lock-free, so freeing a region while the queue lives
+ * would let a later submit in that address range pass validation). */
 int	lcb_hash_queue_register(lcb_hash_queue_p q, const void *base, size_t size);
 
 /* Seal the open batch now (returns at once). */

@@ -188,7 +188,8 @@ using lds_u8 = __attribute__((address_space(3))) const uint8_t;
 constexpr int kGostLpsFence = LCB_GOST_FENCE;
 using lds_u64 = __attribute__((address_space(3))) const uint64_t;
 
-struct GostRot : GostNaturalOrder {
+template <int kFence>
+struct GostRotF : GostNaturalOrder {
     lds_u8* L;
     // Byte j & 3 of offp[j >> 2] = (8c + ((j' + r) & 7)) * 8 (< 256): the lane's
     // bank-pair offsets for the 8 steps, packed 4 to a VGPR (v_perm picks the
@@ -245,10 +246,13 @@ struct GostRot : GostNaturalOrder {
             // Scheduling fence after every kGostLpsFence output words: bounds
             // the ds_read lookahead, which otherwise grows until the 128-VGPR
             // budget of the 4-waves-per-SIMD kernels spills (kernel_resources test).
-            if (kGostLpsFence && (i + 1) % kGostLpsFence == 0) __builtin_amdgcn_sched_barrier(0);
+            if (kFence && (i + 1) % kFence == 0) __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
+// The Sigma-in-LDS kernels (HMAC, keyed) keep the fence; the two-pass plain
+// kernel (no Sigma live through the chain) fits 128 VGPRs without it.
+using GostRot = GostRotF<kGostLpsFence>;
 
 // Fills the 64 KiB rotated image (every thread, then barrier).
 __device__ __forceinline__ void gost_stage_rot(uint64_t* lds) {
@@ -432,6 +436,16 @@ struct Gost {
         if constexpr (kSgLds == 8) gost_g(h, 0, ml, T, sgl, kSgStride);   // g_0(h, Sigma), h ^ Sigma in the Sigma slots
         else gost_g(h, 0, ml, T);   // g_0(h, Sigma)
     }
+    // g_N alone (the two-pass form, gost_run2): Sigma is added up afterwards.
+    template <class Tab>
+    __device__ __forceinline__ void chain(const uint32_t* w, uint64_t bits, const Tab& T) {
+        uint64_t m[8], ml[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+        T.to_lane(ml, m);
+        gost_g(h, get_n(), ml, T);
+        set_n(get_n() + bits);
+    }
     template <class Tab>
     __device__ __forceinline__ void digest_words(uint32_t* out, const Tab& T) const {
         constexpr int first = 8 - kDigest / 8;  // last D bytes of h
@@ -470,9 +484,17 @@ struct Gost {
 
 // Message sources of gost_run: whole 64-B block j (j < nfull) and the
 // zero-filled tail of r = rem() < 64 bytes (tail_n), as raw LE words.
+// opaque(): the same source with its pointers passed through an empty asm,
+// so a second pass's loads are not merged with the first pass's (which would
+// keep the first pass's tail block live across the chain: 104 B/lane spilled).
+__device__ __forceinline__ const uint8_t* opaque_ptr(const uint8_t* p) {
+    asm volatile("" : "+v"(p));
+    return gptr(p);   // still global memory: global_load, not flat_load
+}
 struct GostPlainSrc {   // msg[0, len)
     const uint8_t* p;
     uint64_t len;
+    __device__ __forceinline__ GostPlainSrc opaque() const { return {opaque_ptr(p), len}; }
     __device__ __forceinline__ uint64_t nfull() const { return len >> 6; }
     __device__ __forceinline__ uint32_t rem() const { return (uint32_t)(len & 63u); }
     __device__ __forceinline__ void block(uint64_t j, uint32_t w[16]) const { load_full64(p + 64 * j, w); }
@@ -483,6 +505,7 @@ struct GostVirtSrc {    // A[0, la) || B[0, lb) (keyed batches), nothing copied
     uint64_t la;
     const uint8_t* B;
     uint64_t lb;
+    __device__ __forceinline__ GostVirtSrc opaque() const { return {opaque_ptr(A), la, opaque_ptr(B), lb}; }
     __device__ __forceinline__ uint64_t nfull() const { return (la + lb) >> 6; }
     __device__ __forceinline__ uint32_t rem() const { return (uint32_t)((la + lb) & 63u); }
     __device__ __forceinline__ void block(uint64_t j, uint32_t w[16]) const {
@@ -512,6 +535,68 @@ __device__ __forceinline__ void gost_run(G& st, const Src& src, const Tab& T) {
     const uint32_t rem = src.rem();
     src.tail_n(w, rem);
     st.finish(w, rem, T);
+}
+
+// Sigma += m mod 2^512 on a register Sigma (gost3411-2012.h:996-1013).
+__device__ __forceinline__ void gost_sigma_add(uint64_t sg[8], const uint32_t w[16]) {
+    uint32_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t m = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+        const uint64_t s1 = sg[i] + m;
+        const uint32_t c1 = s1 < m;
+        const uint64_t s2 = s1 + carry;
+        carry = c1 | (s2 < s1);
+        sg[i] = s2;
+    }
+}
+
+// The two-pass form of gost_run (plain batches, Sigma starting at zero):
+// Sigma = the sum of the message's blocks is independent of the g_N chain
+// (gost3411-2012.h:1129-1142: Sigma += m beside h = g_N(h, m)), so the chain
+// runs first with no Sigma at all -- whole blocks, the tail || 0x01 block,
+// then g_0(h, N) (:1836) -- and a second pass over the message adds Sigma up
+// from the bytes again (re-read: L2 / Infinity-Cache resident by then, the
+// kernel is LDS-bound at ~0.04 of HBM) right before the last g_0(h, Sigma)
+// (:1837).  Sigma costs no VGPRs and no LDS through the 19 g's of a 1 KiB
+// message, and nothing is live across g_0(h, N) but h.
+template <class G, class Src, class Tab>
+__device__ __forceinline__ void gost_run2(G& st, const Src& src, const Tab& T) {
+    uint32_t w[16];
+    const uint64_t nfull = src.nfull();
+    for (uint64_t j = 0; j < nfull; ++j) {
+        src.block(j, w);
+        st.chain(w, 512, T);
+    }
+    const uint32_t rem = src.rem();
+    src.tail_n(w, rem);
+    put_byte(w, rem, 0x01u);
+    st.chain(w, (uint64_t)rem * 8u, T);
+    {
+        uint64_t m[8], ml[8];
+        m[0] = st.get_n();
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m[i] = 0;
+        T.to_lane(ml, m);
+        gost_g(st.h, 0, ml, T);                   // g_0(h, N)
+    }
+    uint64_t sg[8], sl[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sg[i] = 0;
+    const Src s2 = src.opaque();
+    for (uint64_t j = 0; j < nfull; ++j) {
+        s2.block(j, w);
+        gost_sigma_add(sg, w);
+    }
+    // The tail's byte masks re-formed from an opaque copy of rem: else they
+    // are computed once and kept (spilled) across the chain.
+    uint32_t r2 = rem;
+    asm volatile("" : "+v"(r2));
+    s2.tail_n(w, r2);
+    put_byte(w, r2, 0x01u);
+    gost_sigma_add(sg, w);
+    T.to_lane(sl, sg);
+    gost_g(st.h, 0, sl, T);                       // g_0(h, Sigma)
 }
 
 // HMAC outer pass (gost3411-2012.h:1902-1934): the D-byte inner digest dw

@@ -40,7 +40,7 @@ __device__ __forceinline__ void settle_words(uint32_t (&w)[N]) {
 }
 
 // ------------------------------------------------------------------ GOST
-// One 1024-thread workgroup per CU (16 waves: four per SIMD, so at most 128
+// HMAC and keyed batches: one 1024-thread workgroup per CU (16 waves: four per SIMD, so at most 128
 // VGPRs per lane) sharing ONE 64 KiB rotated LPS image (gost_device.hpp
 // GostRot), and every lane's Sigma in the LDS beside it (64 KiB, Gost<k256,
 // kGostThreads>): 128 KiB of the CU's 160.  Round 2 ran two 512-thread
@@ -63,8 +63,8 @@ constexpr int kGostSgLds = kGostThreads >= 1024 ? 8 : 4;
     for (uint64_t base = (uint64_t)blockIdx.x * kGostThreads; base < (a).count;                      \
          base += (uint64_t)gridDim.x * kGostThreads)                                                 \
         if (base + threadIdx.x < (a).count)
-template <bool k256, bool kHmac>
-__global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
+template <bool k256>
+__global__ __launch_bounds__(kGostThreads) void gost_hmac_kernel(KArgs a) {
     __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
     __shared__ __attribute__((aligned(16))) uint64_t Sg[(kGostSgLds + (kGostSgLds == 8)) * kGostThreads];  // Sigma of every lane
     gost_stage_rot(Timg);
@@ -78,19 +78,48 @@ __global__ __launch_bounds__(kGostThreads) void gost_batch_kernel(KArgs a) {
     G st;
     st.bind_sigma((lds_u64w*)Sg);
     uint32_t dw[G::kDigest / 4];
-    if (kHmac) {
-        st.load(a.mid, T);   // state after K ^ ipad; the outer pass from K ^ opad
-        gost_run(st, GostPlainSrc{msg, len}, T);
-        st.digest_words(dw, T);
-        gost_outer(st, dw, a.mid + kMidWords, T);
-    } else {
-        st.init();
-        gost_run(st, GostPlainSrc{msg, len}, T);
-    }
+    st.load(a.mid, T);   // state after K ^ ipad; the outer pass from K ^ opad
+    gost_run(st, GostPlainSrc{msg, len}, T);
+    st.digest_words(dw, T);
+    gost_outer(st, dw, a.mid + kMidWords, T);
     st.digest_words(dw, T);
     settle_words<G::kDigest / 4>(dw);
     store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
     }
+}
+
+// Plain GOST batches: the two-pass form (gost_run2: Sigma added up by a
+// second pass over the message after the g_N chain), so neither the LDS nor
+// the VGPRs hold Sigma through the chain and the LDS holds only the 64 KiB
+// rotated image; an ordinary grid of 512-thread workgroups (one message per
+// lane, two workgroups per CU at 4 waves per SIMD, no LPS scheduling fence).
+// Measured against the persistent 1,024-thread Sigma-in-LDS form (the HMAC
+// and keyed kernels below), same box, 1M x 1 KiB (profiles/r4_gost_ab.txt):
+// 2.76-2.80 against 3.02-3.04 ms.  The persistent one-workgroup-per-CU grid
+// keeps all 16 waves of a CU in step, so they wait on their block loads
+// together while the CU's LDS, which bounds GOST, idles; independent
+// workgroups drift apart.  (Persistent 2-pass 2.93 ms, 1,024-thread
+// workgroups 2.93 ms, block prefetch by LDS-DMA 3.14 ms.)
+constexpr int kGostPlainThreads = 512;
+template <bool k256>
+__global__ __launch_bounds__(kGostPlainThreads, 4) void gost_plain2_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
+    gost_stage_rot(Timg);
+    GostRotF<0> T;
+    T.init((lds_u8*)Timg);
+    const uint64_t base = (uint64_t)blockIdx.x * kGostPlainThreads;
+    if (base + threadIdx.x >= a.count) return;
+    uint64_t idx, len;
+    const uint8_t* msg;
+    msg_at(a, base + threadIdx.x, idx, msg, len);
+    using G = Gost<k256>;
+    G st;
+    uint32_t dw[G::kDigest / 4];
+    st.init();
+    gost_run2(st, GostPlainSrc{msg, len}, T);
+    st.digest_words(dw, T);
+    settle_words<G::kDigest / 4>(dw);
+    store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
 }
 
 // Keyed GOST batches (see md_keyed_kernel).
@@ -219,10 +248,10 @@ __global__ __launch_bounds__(256) void gost_hmac_prep_kernel(KeyBlock kb, const 
 // Persistent grid: as many workgroups as fit on the chip at once (the LDS of
 // the image + Sigma and the VGPRs decide how many per CU).
 template <class K>
-static dim3 gost_grid(K kern, uint64_t count) {
-    const uint64_t need = (count + kGostThreads - 1) / kGostThreads;
+static dim3 gost_grid(K kern, uint64_t count, int threads = kGostThreads) {
+    const uint64_t need = (count + threads - 1) / threads;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kGostThreads, 0) != hipSuccess || per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess || per_cu <= 0)
         per_cu = 1;
     const uint64_t slots = (uint64_t)per_cu * device_cu_count();
     return dim3((unsigned)(need < slots ? need : slots));
@@ -230,11 +259,11 @@ static dim3 gost_grid(K kern, uint64_t count) {
 template <bool k256>
 void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
     if (hmac) {
-        auto k = gost_batch_kernel<k256, true>;
+        auto k = gost_hmac_kernel<k256>;
         hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
     } else {
-        auto k = gost_batch_kernel<k256, false>;
-        hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
+        const dim3 g((unsigned)((a.count + kGostPlainThreads - 1) / kGostPlainThreads));
+        hipLaunchKernelGGL(gost_plain2_kernel<k256>, g, dim3(kGostPlainThreads), 0, s, a);
     }
 }
 template <bool k256, int kMode>

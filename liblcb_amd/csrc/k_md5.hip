@@ -5,3 +5,13 @@
 namespace lcbgpu {
 LCB_MD_FAMILY(Md5, md5)
 }  // namespace lcbgpu
+
+#ifdef LCB_TILE_TRACE
+// Diagnostic builds only: where the tile and fixed-stride kernels record
+// their per-tile / per-wave timing (NULL: off).
+extern "C" int lcb_debug_tile_trace(void* tiles, void* fixed) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lcbgpu::g_tile_trace), &tiles, sizeof tiles) != hipSuccess) return 5;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lcbgpu::g_fixed_trace), &fixed, sizeof fixed) != hipSuccess) return 5;
+    return 0;
+}
+#endif

@@ -118,8 +118,10 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint3
 // (stream-ordered temporaries, no synchronisation).
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     uint32_t* work = nullptr;
-    // The bucketing permutation holds message indices as uint32.
-    if (a.lengths && a.order == nullptr && a.count > UINT32_MAX) return EINVAL;
+    // The bucketing permutation holds message indices as uint32 and, padded
+    // per key to whole tiles, up to 63 pad entries (kOrderPad = 2^32 - 1) per
+    // key: its length, the scan and the tile count must stay below 2^32.
+    if (a.lengths && a.order == nullptr && a.count >= kBucketMaxCount) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
         // work: [key histogram | key fill counters | tile-queue head | tile count | order]
         const size_t bytes = bucket_words(a.count) * sizeof(uint32_t);

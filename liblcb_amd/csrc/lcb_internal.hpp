@@ -75,6 +75,8 @@ constexpr uint32_t kOrderPad = 0xffffffffu;
 constexpr uint64_t kBucketPadRatio = 16;
 // uint32 words of bucketing scratch for a batch of `count` messages
 // ([work | order], order padded).
+// Largest ragged batch the uint32 permutation can describe, pads included.
+constexpr uint64_t kBucketMaxCount = 0xffffffffull - 63ull * kBucketKeys;
 inline size_t bucket_words(uint64_t count) { return (size_t)kBucketWork + count + 63ull * kBucketKeys; }
 
 // CRC-32 variants travel through the batch machinery as alg ids

@@ -82,6 +82,38 @@ __global__ __launch_bounds__(256, kPf ? 1 : H::kOcc) void md_batch_kernel(KArgs 
 // 128-B line (each streamed line is one cache line, read once); default
 // otherwise, so the second cache line of a straddling 128-B line is still
 // in L2 when the record's next line asks for it.
+// LCB_TILE_TRACE (diagnostic builds only, tools/build_variant.sh): lane 0
+// of every wave records, per tile, 8 words at g_tile_trace[8 t] -- the
+// 100 MHz real-time clock at the tile's start, after its geometry, at its
+// first and last take and after its digests, the hardware id, the tile's
+// line count | wave id << 16, and the shader cycles over the tile
+// (tools/tile_trace.py reads them).  The fixed-stride kernel records the
+// same per wave at g_fixed_trace[8 w].  Vector stores only.
+#ifdef LCB_TILE_TRACE
+__device__ uint64_t* g_tile_trace;
+__device__ uint64_t* g_fixed_trace;
+__device__ __forceinline__ uint64_t trace_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t trace_hwid() {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return (uint64_t)hw | ((uint64_t)xcc << 32);
+}
+struct TileTrace {
+    uint64_t w[8];
+    __device__ __forceinline__ void mark(int i) { w[i] = trace_now(); }
+    __device__ __forceinline__ void put(uint64_t* buf, uint64_t idx, uint32_t lane) {
+        if (buf && lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) buf[idx * 8 + i] = w[i];
+        }
+    }
+};
+#define LCB_TRACE(...) __VA_ARGS__
+#else
+#define LCB_TRACE(...)
+#endif
+
 template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
@@ -89,6 +121,8 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
+    LCB_TRACE(TileTrace tr; const uint64_t trw = wave_first / 64; const uint64_t trc = __builtin_amdgcn_s_memtime();
+              tr.mark(0); tr.w[1] = tr.w[0]; tr.w[5] = trace_hwid(); tr.w[6] = a.fixed_len / 128;)
     // A partial last wave moves back over its predecessor's records (count >=
     // 64, fixed_stride_lines) and stores only its own: no per-lane clamping.
     const uint64_t last = a.count - 1;
@@ -109,6 +143,7 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
         ls.take(w, w + 16);                 // line L -> VGPRs, its buffer free again
+        LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == nlines) tr.mark(3);)
         if (L + 1 < nlines) ls.issue<kAux>(L + 1);
         if constexpr (H::kBlock == 128) {
             st.compress(w);                 // one SHA-384/512 block per line
@@ -134,6 +169,8 @@ __global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
         o.digest_words(dw);
     }
     store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
+    LCB_TRACE(tr.mark(4); tr.w[7] = __builtin_amdgcn_s_memtime() - trc;
+              tr.put(g_fixed_trace, trw, lane == skip ? 0u : 1u);)
 }
 
 }  // namespace lcbgpu

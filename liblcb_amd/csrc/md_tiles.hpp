@@ -1,12 +1,15 @@
 // md_tiles.hpp — the persistent tile kernel of bucketed ragged MD-family
-// batches (64-byte-block hashes: MD5), included by md_kernels.hpp.
+// batches (the 64-byte-block hashes: MD5, SHA-1, SHA-224/256), included by
+// md_kernels.hpp.
 //
 // A length-bucketed batch (lcb_kernels.hip launch_bucketing: `order` lists
 // messages by key = length class x start phase, longest class first, every
 // key's run padded to whole tiles for a large batch) is cut into TILES of 64
 // consecutive `order` entries; one wave hashes one tile at a time, lane =
-// message.  Workgroups of 4 waves, 5 per CU (each wave owns an 8 KiB LDS
-// slab: the whole 160 KiB), at most 96 VGPRs.  Every wave's first tile is
+// message.  Workgroups of 4 waves (each wave owns an 8 KiB LDS slab), at
+// most kTileWgPerCu = 4 per CU: MD5 at 108-123 VGPRs runs 4 waves per SIMD
+// (H::kTileOcc), SHA-1 / SHA-224/256 at 156-194 VGPRs run 2 (they spill at
+// 3; being VALU-bound they lose nothing by it).  Every wave's first tile is
 // static (its global wave id), later ones come from a device-scope atomic
 // queue head; every wave leaves once the queue is past the last tile, so the
 // grid drains.
@@ -67,9 +70,14 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
+// The key of message idx.  The clamp never fires: lcb_hash_batch_keyed
+// rejects an index >= nkeys with EINVAL before any batch kernel runs (host
+// mode on the host, device mode by key_index_check_kernel, lcb_kernels.hip,
+// whose flag is read before the batch is launched); it only keeps the
+// address inside the key table by construction.
 __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
-    return k < a.nkeys ? k : a.nkeys - 1;   // never out of range: lcb_hash_batch_keyed checked the indices
+    return k < a.nkeys ? k : a.nkeys - 1;
 }
 
 // One lane's record of a tile.  A pad entry (kOrderPad) takes lane 0's
@@ -143,19 +151,6 @@ __device__ __forceinline__ void tile_shift(const uint32_t* c, const uint32_t* y,
         w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
 }
-// Dispatch on the tile's (wave-uniform) R.  R passes through an empty asm at
-// every call so the compiler does not clone the whole line loop per R.
-__device__ __forceinline__ void tile_assemble(uint32_t R, const uint32_t* c, const uint32_t* y, uint32_t sh,
-                                              uint32_t w[16]) {
-    asm volatile("" : "+s"(R));
-    switch (R) {
-    case 0: tile_shift<0>(c, y, sh, w); break;
-    case 1: tile_shift<1>(c, y, sh, w); break;
-    case 2: tile_shift<2>(c, y, sh, w); break;
-    default: tile_shift<3>(c, y, sh, w); break;
-    }
-}
-
 // The carry block's first 16 words: word j of the lane's rotated stream is
 // still the carry (dwords 16..31 of line L - 1) while its chunk j >> 2 + m
 // lies below 4, else it wrapped round into line L (y[16 + j]).
@@ -218,12 +213,21 @@ __device__ __forceinline__ void tile_init(H& st) {
     }
 }
 
+// The HMAC mid-state pointer re-defined per use: its words (wave-uniform
+// for one key) are loaded per tile instead of being hoisted out of the
+// persistent loop into 8 SGPRs held all along (which spilled SGPRs).
+__device__ __forceinline__ const uint32_t* tile_mid(const KArgs& a) {
+    const uint32_t* mid = a.mid;
+    asm volatile("" : "+s"(mid));
+    return gptr(mid);
+}
+
 template <class H, int kMode>
 __device__ __forceinline__ void tile_finish(const KArgs& a, H& st, const TileRec& r) {
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kMode == kTileHmac || kMode == kTileKeyedHmac) {
-        const uint32_t* mid = gptr(a.mid);
+        const uint32_t* mid = tile_mid(a);
         if (kMode == kTileKeyedHmac) mid += (uint64_t)key_of(a, r.idx) * 2 * kMidWords;
         H o;
         load_words(o.s, mid + kMidWords);   // state after K ^ opad
@@ -240,7 +244,7 @@ __device__ __forceinline__ void tile_state(const KArgs& a, const TileRec& r, H& 
     m.K = nullptr;
     m.kl = 0;
     if (kMode == kTileHmac || kMode == kTileKeyedHmac) {
-        const uint32_t* mid = gptr(a.mid);
+        const uint32_t* mid = tile_mid(a);
         if (kMode == kTileKeyedHmac) mid += (uint64_t)key_of(a, r.idx) * 2 * kMidWords;
         load_words(st.s, mid);              // state after K ^ ipad
         m.prefix = H::kBlock;
@@ -266,6 +270,49 @@ __device__ __forceinline__ void md_tile_direct(const KArgs& a, const TileRec& r)
     tile_finish<H, kMode>(a, st, r);
 }
 
+// Wave-level reductions by DPP (no LDS round trips): the 16-lane rows by
+// quad_perm xor 1, xor 2, row_half_mirror and row_mirror (each lane ends
+// with its row's result), the four rows combined on the SALU.  The tile
+// geometry's seven reductions were 6-deep ds_bpermute chains (r3: ~2 us per
+// tile with no line in flight, tools/tile_trace.py).
+constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowHalfMirror = 0x141, kDppRowMirror = 0x140;
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v, uint32_t ident) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, kCtrl, 0xf, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, uint32_t ident, Op op) {
+    v = op(v, dpp_mov<kDppQuadXor1>(v, ident));
+    v = op(v, dpp_mov<kDppQuadXor2>(v, ident));
+    v = op(v, dpp_mov<kDppRowHalfMirror>(v, ident));
+    v = op(v, dpp_mov<kDppRowMirror>(v, ident));
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return op(op(r0, r1), op(r2, r3));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return wave_reduce(v, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    return wave_reduce(v, ~0u, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+}
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
+    return (int32_t)wave_reduce((uint32_t)v, 0x80000000u,
+                                [](uint32_t x, uint32_t y) { return (int32_t)x > (int32_t)y ? x : y; });
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+    return (int32_t)wave_reduce((uint32_t)v, 0x7fffffffu,
+                                [](uint32_t x, uint32_t y) { return (int32_t)x < (int32_t)y ? x : y; });
+}
+// OR over the lane's group of 8 (lanes 8q .. 8q + 7): quad xor 1, xor 2,
+// then row_half_mirror pairs the two quads.
+__device__ __forceinline__ uint32_t group8_or(uint32_t v) {
+    v |= dpp_mov<kDppQuadXor1>(v, 0u);
+    v |= dpp_mov<kDppQuadXor2>(v, 0u);
+    v |= dpp_mov<kDppRowHalfMirror>(v, 0u);
+    return v;
+}
+
 // The tile's line stream: line L of the 64 records moves into the wave's
 // 8 KiB slab with 8 global_load_lds_dwordx4.  Lane group q (lanes 8q ..
 // 8q + 7) carries, in instruction g, the whole 128-B cache line L of record
@@ -289,11 +336,7 @@ struct TileGatherStream {
     uint32_t voff[8];       // instruction g: this lane's chunk of record 8 (lane >> 3) + g, bytes from tb
     // The rotations of the lane's group of 8 records, 2 bits each.
     __device__ __forceinline__ static uint32_t group_rot(uint32_t m, uint32_t ln) {
-        uint32_t mpk = m << (2u * (ln & 7u));
-        mpk |= (uint32_t)__shfl_xor((int)mpk, 1, 64);
-        mpk |= (uint32_t)__shfl_xor((int)mpk, 2, 64);
-        mpk |= (uint32_t)__shfl_xor((int)mpk, 4, 64);
-        return mpk;
+        return group8_or(m << (2u * (ln & 7u)));
     }
     __device__ __forceinline__ void init(const uint8_t* tile_base, uint32_t rel, uint32_t m, uint32_t ln,
                                          uint8_t* my_slab) {
@@ -329,10 +372,7 @@ struct TileGatherStream {
         asm volatile("" : "+v"(ln));
         int n = (int)lastc - 8 * (int)L + 1;                    // valid chunks of line L
         n = n < 0 ? 0 : (n > 8 ? 8 : n);
-        uint32_t nv = (uint32_t)n << (4u * (ln & 7u));
-        nv |= (uint32_t)__shfl_xor((int)nv, 1, 64);
-        nv |= (uint32_t)__shfl_xor((int)nv, 2, 64);
-        nv |= (uint32_t)__shfl_xor((int)nv, 4, 64);
+        const uint32_t nv = group8_or((uint32_t)n << (4u * (ln & 7u)));
         const uint32_t mpk = group_rot(m, ln);
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -363,7 +403,8 @@ struct TileGatherStream {
 
 template <class H, int kMode, int kR>
 __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
-                                               TileClaim& cl, uint64_t ntiles, uint32_t norder, uint32_t nwaves) {
+                                               TileClaim& cl, uint64_t ntiles, uint32_t norder, uint32_t nwaves
+                                               LCB_TRACE(, TileTrace& tr)) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
     const uint32_t sh = p32 & 3u;
     const uint32_t off = p32 & 127u;              // stream offset of the record's first byte
@@ -383,45 +424,34 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     const uint64_t end = off + len;                          // record end, in stream bytes
     const uint32_t nblk = (uint32_t)((m_.total + 8u) >> 6) + 1u;
     const uint32_t nf = r.len >> 6;
-    uint32_t NL = (uint32_t)((end + 127u) >> 7), NS = (uint32_t)(end >> 7), NB = nblk + h;
-    uint32_t LF = (nf + h + 1u) >> 1, NF = nf;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {                       // wave max / min (xor butterfly)
-        NL = max(NL, (uint32_t)__shfl_xor((int)NL, d, 64));
-        NB = max(NB, (uint32_t)__shfl_xor((int)NB, d, 64));
-        NS = min(NS, (uint32_t)__shfl_xor((int)NS, d, 64));
-        LF = min(LF, (uint32_t)__shfl_xor((int)LF, d, 64));
-        NF = min(NF, (uint32_t)__shfl_xor((int)NF, d, 64));
-    }
-    NL = __builtin_amdgcn_readfirstlane(NL);
-    NB = __builtin_amdgcn_readfirstlane(NB);
-    NS = __builtin_amdgcn_readfirstlane(NS);
-    LF = __builtin_amdgcn_readfirstlane(LF);
-    NF = __builtin_amdgcn_readfirstlane(NF);
+    const uint32_t NL = wave_max_u32((uint32_t)((end + 127u) >> 7)), NS = wave_min_u32((uint32_t)(end >> 7));
+    const uint32_t NB = wave_max_u32(nblk + h), NF = wave_min_u32(nf);
+    uint32_t LF = wave_min_u32((nf + h + 1u) >> 1);
     if (LF > NL) LF = NL;
     // The tile's stream bases: 32-bit offsets from the lowest (saddr form)
-    // when the tile spans less than 4 GiB, else the per-lane loop.
+    // when the tile spans less than 4 GiB, else the per-lane loop.  Bases
+    // are compared as signed 128-B line deltas from lane 0's, so each bound
+    // is one 32-bit reduction.
     const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off;
-    uint64_t lo = base, hi = base;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d, 64));
-        hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d, 64));
-    }
-    lo = readfirstlane64(lo);
-    hi = readfirstlane64(hi);
-    if (hi - lo + (uint64_t)(NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
+    const uint64_t b0 = readfirstlane64(base);
+    const int64_t d = (int64_t)(base - b0);
+    const bool near = d > -(1ll << 38) && d < (1ll << 38);
+    const int32_t dl = (int32_t)(d >> 7);
+    const int32_t dmin = wave_min_i32(dl), dmax = wave_max_i32(dl);
+    const uint64_t lo = b0 + (uint64_t)((int64_t)dmin * 128);
+    if (!__all(near) || ((uint64_t)(uint32_t)(dmax - dmin) + NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
         if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m_.K, m_.kl, 0);
         else md_message(st, r.p, r.len, m_.prefix);
         tile_finish<H, kMode>(a, st, r);
         return;
     }
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
+    LCB_TRACE(tr.mark(1); tr.w[6] = NL;)
     // No lane's chunks rotated (every start on a 64-B half line, as in C4):
     // the carry needs no merge (wave-uniform).
     const bool rotated = !__all(m == 0);
     TileGatherStream ls;
-    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(base - lo), m, lane, slab);
+    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(dl - dmin) * 128u, m, lane, slab);
     auto issue = [&](uint32_t L) {
         if (L >= NS) ls.issue_masked(L, lastc, rot());
         else ls.issue(L);
@@ -440,6 +470,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     for (; L < LF; ++L) {
         uint32_t y[32];
         ls.take(y);
+        LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
         if (L + 1 < LE) issue(L + 1);
         if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         uint32_t w[16];
@@ -468,6 +499,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         uint32_t y[32];
         if (L < NL) {
             ls.take(y);
+            LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
             if (L + 1 < NL) issue(L + 1);
             if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         } else {
@@ -503,6 +535,8 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
     if (cl.t < ntiles) tile_rec_load(a, tile_entry(a, cl.t, lane, norder), cl.r);
     while (cl.t < ntiles) {
         const TileRec r = cl.r;
+        LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0; const uint64_t trt = cl.t;
+                  const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
         cl.stage = 0;
         // The lane id re-defined per tile: what the tile derives from it
         // (bpermute addresses, slab slots, chunk numbers) is formed per tile
@@ -517,14 +551,16 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
             // word selection is static (no per-call dispatch and the register
             // moves that merge its cases).
             switch (R) {
-            case 0: md_tile_stream<H, kMode, 0>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
-            case 1: md_tile_stream<H, kMode, 1>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
-            case 2: md_tile_stream<H, kMode, 2>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
-            default: md_tile_stream<H, kMode, 3>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves); break;
+            case 0: md_tile_stream<H, kMode, 0>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
+            case 1: md_tile_stream<H, kMode, 1>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
+            case 2: md_tile_stream<H, kMode, 2>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
+            default: md_tile_stream<H, kMode, 3>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
             }
         } else {
             md_tile_direct<H, kMode>(a, r);
         }
+        LCB_TRACE(tr.mark(4); tr.w[6] |= ((uint64_t)blockIdx.x * kTileWaves + wv) << 16;
+                  tr.w[7] = __builtin_amdgcn_s_memtime() - trc; tr.put(g_tile_trace, trt, lane);)
         while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
     }
 }

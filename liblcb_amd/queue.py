@@ -72,6 +72,8 @@ class HashQueue:
         if hasattr(area, "data_ptr"):
             if not area.is_pinned():
                 raise ValueError("torch tensor must be pinned")
+            if not area.is_contiguous():
+                raise ValueError("area must be contiguous")   # else numel*size is not its byte extent
             p, n = area.data_ptr(), area.numel() * area.element_size()
         else:
             a = np.asarray(area)

@@ -124,3 +124,25 @@ def test_multi_errors(gpu):
     with pytest.raises(gpu.LcbHashError) as e:
         gpu.hash_batch_multi([0, 99], 1, d, count=1, fixed_len=16)
     assert e.value.errno == errno.ENODEV
+
+
+@pytest.mark.gpu
+def test_multi_c5_eight_parts_copy(gpu):
+    """C5 through lcb_hash_batch_multi with devs = {0 x 8} and the peer-copy
+    path forced (LCB_HASH_F_COPY_PARTS): 8M x 1 KiB split into 8 parts, each
+    remote part's span copied and hashed beside the others, digests gathered
+    back in order -- equal to the reference's digest-of-digests
+    (tests/golden/large.json C5_8M_x_1k)."""
+    import hashlib
+    import json
+    import os
+    import torch
+    large = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "large.json")))
+    fx = large["C5_8M_x_1k"]
+    n = fx["count"]
+    data = gpu.gen_synthetic(large["seed"], n * 1024)
+    got = gpu.hash_batch_multi([0] * 8, 1, data, count=n, stride=1024, fixed_len=1024, copy_parts=True)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest() == fx["algs"]["md5"]["dod"]
+    del data, got
+    torch.cuda.empty_cache()
