@@ -192,16 +192,33 @@ def time_alg(alg, data, digests, count, steps, warmup, world, key=None):
     return max_over_ranks(t, world), kms
 
 
+def counters_current(rec):
+    """True when a committed counter record (profiles/pmc_<alg>.json,
+    valu_counts.json) was measured on the kernel code the loaded library
+    runs: the sha256 of that kernel's machine code in the library
+    (tools/codestamp.py) equals the record's stamp.  A record of an earlier
+    build (or without a stamp) is never reported against this one."""
+    from liblcb_amd._lib import LIB_PATH
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import codestamp
+    try:
+        return bool(rec.get("kernel_symbol")) and codestamp.stamp_of(LIB_PATH, rec["kernel_symbol"]) == \
+            rec.get("code_sha256")
+    except (OSError, ValueError):
+        return False
+
+
 def pmc_traffic(alg, count):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, corrected
     as MI355X_MICROARCH.md prescribes (FETCH_SIZE reads 1/2 of a wide
-    coalesced stream on gfx950: doubled; WRITE_SIZE exact; both in KiB)."""
+    coalesced stream on gfx950: doubled; WRITE_SIZE exact; both in KiB);
+    None unless the record's code stamp matches the loaded kernel."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % ALG_NAMES[alg])
     if not os.path.exists(path):
         return None
     try:
         j = json.load(open(path))
-        if j.get("count") != count or j.get("msg_len") != MSG_LEN:
+        if j.get("count") != count or j.get("msg_len") != MSG_LEN or not counters_current(j):
             return None
         return float(j["hbm_bytes_per_launch"])
     except (ValueError, KeyError):
@@ -216,13 +233,17 @@ VALU_CLOCK_HZ = 2.4e9    # MI355X max engine clock (MI355X_MICROARCH.md)
 def valu_floor_ms(alg, count):
     """VALU issue floor of one launch on the bench workload: the committed
     SQ_INSTS_VALU count (profiles/valu_counts.json, rocprofv3 --pmc) x 4
-    cycles / (1,024 SIMDs x 2.4 GHz).  None without a count for this shape."""
+    cycles / (1,024 SIMDs x 2.4 GHz).  None without a count for this shape,
+    or when the count's code stamp does not match the loaded kernel."""
     path = os.path.join(ROOT, "profiles", "valu_counts.json")
     try:
         j = json.load(open(path))
         if j.get("count") != count or j.get("msg_len") != MSG_LEN:
             return None
-        n = float(j["algs"][ALG_NAMES[alg]]["SQ_INSTS_VALU"])
+        rec = j["algs"][ALG_NAMES[alg]]
+        if not counters_current(rec):
+            return None
+        n = float(rec["SQ_INSTS_VALU"])
     except (OSError, ValueError, KeyError):
         return None
     return n * VALU_CYCLES / (VALU_SIMDS * VALU_CLOCK_HZ) * 1e3
@@ -255,6 +276,22 @@ def read_probes(data, count, steps=50, warmup=20):
         out[name + "_ms"] = round(ms, 4)
         del sink
     return out
+
+
+def gost_lps_floor_ms(count, steps=10, warmup=3):
+    """GOST's real bound on this box (DESIGN.md 5): the plain GOST kernel's
+    LDS table gathers alone -- lcb_hash_gpu_read_probe LCB_PROBE_GOST_LPS,
+    the kernel's grid, LDS image and occupancy running each lane's 475 LPS
+    (1 KiB message: 19 g x 25) as one chain with no loads, no Sigma.  Mean
+    HIP-event ms per launch."""
+    stream = torch.cuda.current_stream()
+    sink = torch.empty(count, dtype=torch.int32, device="cuda")
+
+    def launch():
+        check(lib().lcb_hash_gpu_read_probe(2, None, count, MSG_LEN, MSG_LEN, sink.data_ptr(), stream.cuda_stream))
+    ms = _event_ms(launch, warmup, steps, stream)
+    del sink
+    return ms
 
 
 def affinity_cpus():
@@ -794,6 +831,15 @@ def main():
                          "kernel_ms": round(km, 4),
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "valu_frac": round(vf / km, 4) if vf else None}
+            if name.startswith("gost"):
+                # GOST is bound by its LDS table gathers, not HBM or VALU:
+                # the gathers alone, same grid and image, beside the kernel.
+                if "lps_chain_ms" not in per.get("gost256", {}):
+                    lps_ms = gost_lps_floor_ms(count)
+                else:
+                    lps_ms = per["gost256"]["lps_chain_ms"]
+                per[name]["lps_chain_ms"] = round(lps_ms, 4)
+                per[name]["lds_frac"] = round(lps_ms / km, 4)
             del dg
         out["per_alg"] = per
         # Batched HMAC (RADIUS needs HMAC-MD5): per call

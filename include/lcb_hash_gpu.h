@@ -215,10 +215,15 @@ int	lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t *dev_out,
  * dev_data 16-B aligned, count >= 64); `dev_sink` receives count uint32.
  * mode LCB_PROBE_LINEAR: coalesced 16-B loads over count * stride bytes
  * (a multiple of 16); `dev_sink` receives lcb_hash_gpu_probe_sink_words()
- * uint32.  Asynchronous on `stream`.  EINVAL on a shape the mode cannot
- * read. */
+ * uint32.  mode LCB_PROBE_GOST_LPS: no memory read at all -- the plain GOST
+ * kernel's table gathers alone (its grid and LDS image; per lane the LPS
+ * count of a fixed_len-byte message as one dependent chain, dev_data
+ * unused): the LDS bound of GOST beside its kernel time; `dev_sink`
+ * receives count uint32.  Asynchronous on `stream`.  EINVAL on a shape the
+ * mode cannot read. */
 #define LCB_PROBE_RECORDS	0
 #define LCB_PROBE_LINEAR	1
+#define LCB_PROBE_GOST_LPS	2
 int	lcb_hash_gpu_read_probe(int mode, const uint8_t *dev_data, size_t count,
 	    uint64_t stride, uint32_t fixed_len, uint32_t *dev_sink, void *stream);
 size_t	lcb_hash_gpu_probe_sink_words(int mode, size_t count);

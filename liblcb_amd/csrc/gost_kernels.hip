@@ -122,6 +122,42 @@ __global__ __launch_bounds__(kGostPlainThreads, 4) void gost_plain2_kernel(KArgs
     store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
 }
 
+// Diagnostic (lcb_hash_gpu_read_probe LCB_PROBE_GOST_LPS): the bound of the
+// plain kernel -- its LDS gathers alone.  The same grid, workgroups, table
+// image and occupancy as gost_plain2_kernel; each lane runs the plain
+// kernel's number of LPS transforms for a fixed_len-byte message (19 g of 25
+// LPS for 1 KiB) as ONE dependent chain (each g's 25 LPS are a chain: t
+// needs the new K), with no block loads, no Sigma and no feed-forward.  The
+// bench reports lds_frac = this time / the kernel's.
+__global__ __launch_bounds__(kGostPlainThreads, 4) void gost_lps_probe_kernel(uint64_t count, uint32_t nlps,
+                                                                              uint32_t* sink) {
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];
+    gost_stage_rot(Timg);
+    GostRotF<0> T;
+    T.init((lds_u8*)Timg);
+    const uint64_t i = (uint64_t)blockIdx.x * kGostPlainThreads + threadIdx.x;
+    if (i >= count) return;
+    uint64_t x[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = 0x9e3779b97f4a7c15ull * (i * 8 + k + 1);
+#pragma unroll 1
+    for (uint32_t r = 0; r < nlps; ++r) {
+        T.lps(o, x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = o[k] ^ (uint64_t)(r + k);   // the chain's round-constant XOR
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc ^= x[k];
+    gptr(sink)[i] = (uint32_t)acc ^ (uint32_t)(acc >> 32);
+}
+
+void launch_gost_lps_probe(uint64_t count, uint32_t fixed_len, uint32_t* sink, hipStream_t s) {
+    const uint32_t nlps = (fixed_len / 64 + 1 + 2) * 25;   // g_N per whole block + tail, g_0 twice
+    hipLaunchKernelGGL(gost_lps_probe_kernel, dim3((unsigned)((count + kGostPlainThreads - 1) / kGostPlainThreads)),
+                       dim3(kGostPlainThreads), 0, s, count, nlps, sink);
+}
+
 // Keyed GOST batches (see md_keyed_kernel).
 template <bool k256, int kMode>
 __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {

@@ -689,7 +689,7 @@ int lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t* dev_out, size
 }
 
 size_t lcb_hash_gpu_probe_sink_words(int mode, size_t count) {
-    if (mode == LCB_PROBE_RECORDS) return count;
+    if (mode == LCB_PROBE_RECORDS || mode == LCB_PROBE_GOST_LPS) return count;
     if (ensure_init()) return 0;
     return (size_t)8 * device_cu_count() * 256;
 }
@@ -697,6 +697,11 @@ size_t lcb_hash_gpu_probe_sink_words(int mode, size_t count) {
 int lcb_hash_gpu_read_probe(int mode, const uint8_t* dev_data, size_t count, uint64_t stride, uint32_t fixed_len,
                             uint32_t* dev_sink, void* stream) {
     if (int rc = ensure_init()) return rc;
+    if (mode == LCB_PROBE_GOST_LPS) {
+        if (!dev_sink || count == 0 || count > UINT32_MAX) return EINVAL;
+        launch_gost_lps_probe(count, fixed_len, dev_sink, reinterpret_cast<hipStream_t>(stream));
+        return map_err(hipGetLastError());
+    }
     if (!dev_data || !dev_sink || count == 0) return EINVAL;
     KArgs a{};
     a.data = dev_data;

@@ -61,11 +61,24 @@ struct KeyBlock {
 constexpr int kBucketClasses = 122;
 constexpr int kBucketPhases = 4;
 constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
-// Bucketing scratch ahead of the permutation: key histogram, per-key fill
-// counters, the tile-queue head, the number of 64-entry tiles (uint32 words).
+// Bucketing scratch ahead of the permutation: per-key totals, a spare
+// block, the tile-queue head, the number of `order` entries (uint32 words).
+// After the permutation: the per-block key counts, their per-block bases
+// (bucket_blocks(count) x kBucketKeys words each) and one 16-bit key per
+// message.
 constexpr int kBucketHead = 2 * kBucketKeys;
 constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
 constexpr int kBucketWork = 2 * kBucketKeys + 2;
+// Messages per bucketing block: count / 1024, clamped to [4096, 8192] (the
+// placement sorts a block's whole chunk in LDS).
+constexpr uint64_t kBucketBlocksTarget = 1024;
+constexpr uint64_t kBucketChunkMin = 4096;
+constexpr uint64_t kBucketChunkMax = 8192;
+inline uint64_t bucket_chunk(uint64_t count) {
+    uint64_t c = (count + kBucketBlocksTarget - 1) / kBucketBlocksTarget;
+    return c < kBucketChunkMin ? kBucketChunkMin : (c > kBucketChunkMax ? kBucketChunkMax : c);
+}
+inline uint64_t bucket_blocks(uint64_t count) { return (count + bucket_chunk(count) - 1) / bucket_chunk(count); }
 // Ragged batches at least this large are bucketed by length first.
 constexpr uint64_t kBucketMinCount = 4096;
 // When every key has enough messages (count >= kBucketPadRatio * 64 * keys
@@ -77,7 +90,10 @@ constexpr uint64_t kBucketPadRatio = 16;
 // ([work | order], order padded).
 // Largest ragged batch the uint32 permutation can describe, pads included.
 constexpr uint64_t kBucketMaxCount = 0xffffffffull - 63ull * kBucketKeys;
-inline size_t bucket_words(uint64_t count) { return (size_t)kBucketWork + count + 63ull * kBucketKeys; }
+inline size_t bucket_order_words(uint64_t count) { return (size_t)count + 63ull * kBucketKeys; }
+inline size_t bucket_words(uint64_t count) {
+    return (size_t)kBucketWork + bucket_order_words(count) + 2 * bucket_blocks(count) * kBucketKeys + (count + 1) / 2;
+}
 
 // CRC-32 variants travel through the batch machinery as alg ids
 // kCrcAlgBase + variant (variant ids of include/lcb_crc32_gpu.h).
@@ -149,6 +165,9 @@ void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint3
 // stream alone over `a`'s records, mode 1 = linear coalesced read of
 // count * stride bytes; sink: one uint32 per record (0) / per thread (1).
 void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s);
+// mode 2: the plain GOST kernel's LDS gathers alone (count lanes, the LPS
+// count of a fixed_len-byte message each); sink: one uint32 per lane.
+void launch_gost_lps_probe(uint64_t count, uint32_t fixed_len, uint32_t* sink, hipStream_t s);
 void gost_table_host(uint64_t* out);
 
 // Shared by the C-ABI TUs (lcb_hash_gpu.cpp).

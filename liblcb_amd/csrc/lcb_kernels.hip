@@ -128,90 +128,205 @@ __device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
     return len_class(gptr(a.lengths)[i]) * kBucketPhases + ((p >> 2) & 3u);
 }
 
-// Few, large blocks (kBucketBlocks x 1024 threads): every block adds its LDS
-// histogram to the global one with one atomic per key it saw, and the
-// atomics on a hot key serialise (one word takes ~88 per us,
-// MI355X_MICROARCH.md): 4096 blocks of 256 cost ~50 us on a 3-length batch.
-constexpr uint32_t kBucketBlocks = 512;
+// A counting sort in three kernels with no global atomics (round 3's two
+// kernels took 13 + 23.5 us on 1M packets, about 7 % of a packet pass, much
+// of it the serialised per-key atomics of 512 blocks on a few hundred
+// counters; profiles/r4_bucketing_ab.txt).  Block b of nb owns the
+// contiguous chunk [b * chunk, (b + 1) * chunk):
+//   bucket_count_kernel  key of every message (16 bits, kept for the last
+//                        pass) and the block's key counts -> cnt[k][b]
+//                        (key-major: one key's counts are contiguous);
+//   bucket_base_kernel   one wave per key: base[k][b] = sum of cnt[k][b' < b]
+//                        (coalesced loads, a wave scan), tot[k] = all of them;
+//   bucket_place_kernel  every block scans the key totals in DESCENDING key
+//                        order (one wave; runs padded to whole tiles for a
+//                        large batch) and places its messages at
+//                        start[k] + base[k][b] + rank (LDS atomics); block 0
+//                        writes the pad entries, the entry count and a zero
+//                        tile-queue head.
+// Messages per thread in one unrolled step of the bucketing kernels (their
+// loads issued together, not one round trip per message).
+constexpr int kBucketUnroll = 4;
 
-__global__ __launch_bounds__(1024) void bucket_hist_kernel(KArgs a, uint32_t* hist) {
+__global__ __launch_bounds__(1024) void bucket_count_kernel(KArgs a, uint64_t chunk, uint32_t nb, uint32_t* cnt,
+                                                           uint16_t* keys) {
     __shared__ uint32_t h[kBucketKeys];
     for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) h[c] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[bucket_key(a, i)], 1u);
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
+    for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
+        uint32_t k[kBucketUnroll];
+#pragma unroll
+        for (int u = 0; u < kBucketUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+            k[u] = i < hi ? bucket_key(a, i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kBucketUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+            if (i < hi) {
+                gptr(keys)[i] = (uint16_t)k[u];
+                atomicAdd(&h[k[u]], 1u);
+            }
+        }
+    }
     __syncthreads();
-    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x)
-        if (h[c]) atomicAdd(&hist[c], h[c]);
+    for (int c = threadIdx.x; c < kBucketKeys; c += blockDim.x) gptr(cnt)[(uint64_t)c * nb + blockIdx.x] = h[c];
 }
 
 static_assert(kBucketKeys <= 1024, "one scan element per thread");
 
-// Block b owns the contiguous chunk [b * chunk, (b + 1) * chunk).  Every block
-// derives the start of each key's run (DESCENDING key order, runs padded to
-// whole tiles when the batch is large) from the global histogram with one
-// 1024-wide LDS scan, counts its own keys, reserves one range per key (fill
-// counter atomics), then places its indices (LDS atomics give the rank inside
-// the block's range).  Block 0 also writes the pad entries and the tile count.
-__global__ __launch_bounds__(1024) void bucket_scatter_kernel(KArgs a, const uint32_t* hist, uint32_t* fill,
-                                                             uint32_t* ntiles, uint32_t* order, uint64_t chunk,
-                                                             bool allow_pad) {
-    __shared__ uint32_t h[kBucketKeys];
-    __shared__ uint32_t base[1024];
+// Inclusive scan of v over the wave (6 ds_bpermute steps).
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= (uint32_t)d) v += u;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void bucket_base_kernel(const uint32_t* cnt, uint32_t nb, uint32_t* base,
+                                                          uint32_t* tot) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= (uint32_t)kBucketKeys) return;   // wave-uniform
+    const uint32_t* c = gptr(cnt) + (uint64_t)k * nb;
+    uint32_t* o = gptr(base) + (uint64_t)k * nb;
+    uint32_t run = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {   // 4 counts per lane per round
+        uint32_t v[4], s = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = b0 + 4 * lane + u;
+            v[u] = b < nb ? c[b] : 0u;
+            s += v[u];
+        }
+        const uint32_t incl = wave_scan_incl(s, lane);
+        uint32_t e = run + incl - s;              // exclusive prefix of this lane's first count
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t b = b0 + 4 * lane + u;
+            if (b < nb) o[b] = e;
+            e += v[u];
+        }
+        run += (uint32_t)__shfl((int)incl, 63, 64);
+    }
+    if (lane == 0) gptr(tot)[k] = run;
+}
+
+// The block sorts its chunk by key in LDS first (local offsets from its own
+// counts), then writes `order` in sorted order: consecutive threads write
+// consecutive entries of one key's run, so a wave's 64 stores cover a few
+// contiguous runs instead of 64 scattered dwords (each a partial-line write).
+static_assert(kBucketChunkMax <= 8192, "a block's chunk sorts in LDS");
+__global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t chunk, uint32_t nb,
+                                                            const uint32_t* cnt, const uint32_t* base,
+                                                            const uint32_t* tot, const uint16_t* keys,
+                                                            uint32_t* work, uint32_t* order, bool allow_pad) {
+    __shared__ uint32_t h[kBucketKeys];        // run start in `order` of this block's entries, per key
+    __shared__ uint32_t loc[kBucketKeys];      // local (sorted) offset per key, then the fill cursor
+    __shared__ uint32_t len_s[kBucketKeys];
+    __shared__ uint32_t sidx[kBucketChunkMax];
+    __shared__ uint16_t skey[kBucketChunkMax];
+    __shared__ uint32_t misc[2];
     const uint32_t t = threadIdx.x;
-    // Scan element t = key kBucketKeys - 1 - t (descending), padded count.
-    const int kt = (int)kBucketKeys - 1 - (int)t;
-    const uint32_t hk = kt >= 0 ? hist[kt] : 0u;
+    // Padded run lengths, then one wave scans them in DESCENDING key order
+    // (the longest class first): lane l owns keys K-1-8l .. K-8-8l; wave 1
+    // scans the block's own counts (ascending: any order works locally).
+    const uint32_t hk = t < (uint32_t)kBucketKeys ? gptr(tot)[t] : 0u;
     const int used = __syncthreads_count(hk != 0);
     const bool pad = allow_pad && a.count >= kBucketPadRatio * 64 * (uint64_t)used;
-    const uint32_t len = pad ? (hk + 63u) & ~63u : hk;
-    base[t] = len;
-    for (int c = t; c < kBucketKeys; c += blockDim.x) h[c] = 0;
+    if (t < (uint32_t)kBucketKeys) len_s[t] = pad ? (hk + 63u) & ~63u : hk;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {     // inclusive scan (Hillis-Steele)
-        const uint32_t v = t >= d ? base[t - d] : 0u;
-        __syncthreads();
-        base[t] += v;
-        __syncthreads();
-    }
-    const uint32_t start = base[t] - len;          // exclusive
-    __syncthreads();
-    if (kt >= 0) {
-        if (blockIdx.x == 0) {
-            for (uint32_t e = start + hk; e < start + len; ++e) order[e] = kOrderPad;
-            if (t == 0) *ntiles = base[1023];   // entries of `order`, pads included
+    constexpr int kPer = (kBucketKeys + 63) / 64;
+    if (t < 64) {
+        uint32_t v[kPer], s = 0;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int k = kBucketKeys - 1 - (kPer * (int)t + u);
+            v[u] = k >= 0 ? len_s[k] : 0u;
+            s += v[u];
         }
-        base[t] = start;                           // base of key kt at scan slot t
+        const uint32_t incl = wave_scan_incl(s, t);
+        uint32_t e = incl - s;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int k = kBucketKeys - 1 - (kPer * (int)t + u);
+            if (k >= 0) h[k] = e;                // start of key k's run
+            e += v[u];
+        }
+        if (t == 63) misc[0] = incl;             // entries of `order`, pads included
+    } else if (t < 128) {
+        const uint32_t l = t - 64;
+        uint32_t v[kPer], s = 0;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int k = kPer * (int)l + u;
+            v[u] = k < kBucketKeys ? gptr(cnt)[(uint64_t)k * nb + blockIdx.x] : 0u;
+            s += v[u];
+        }
+        uint32_t e = wave_scan_incl(s, l) - s;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int k = kPer * (int)l + u;
+            if (k < kBucketKeys) loc[k] = e;
+            e += v[u];
+        }
     }
+    __syncthreads();
+    if (t < (uint32_t)kBucketKeys) {
+        const uint32_t start = h[t];
+        if (blockIdx.x == 0)
+            for (uint32_t e = start + hk; e < start + len_s[t]; ++e) gptr(order)[e] = kOrderPad;
+        // order position of the key's first local entry, minus its local offset
+        h[t] = start + gptr(base)[(uint64_t)t * nb + blockIdx.x] - loc[t];
+    }
+    if (blockIdx.x == 0 && t == 0) {
+        gptr(work)[kBucketNTiles] = misc[0];
+        gptr(work)[kBucketHead] = 0u;            // tile-queue head
+    }
+    __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
-    for (uint64_t i = lo + t; i < hi; i += blockDim.x) atomicAdd(&h[bucket_key(a, i)], 1u);
-    __syncthreads();
-    for (int k = t; k < kBucketKeys; k += blockDim.x) {
-        const uint32_t slot = (uint32_t)(kBucketKeys - 1 - k);
-        if (h[k]) base[slot] += atomicAdd(&fill[k], h[k]);
-        h[k] = 0;
+    // chunk <= kBucketChunkMax (bucket_chunk): the whole chunk sorts in LDS.
+    for (uint64_t i0 = lo + t; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
+        uint32_t k[kBucketUnroll];
+#pragma unroll
+        for (int u = 0; u < kBucketUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+            k[u] = i < hi ? gptr(keys)[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kBucketUnroll; ++u) {
+            const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+            if (i < hi) {
+                const uint32_t p = atomicAdd(&loc[k[u]], 1u);
+                sidx[p] = (uint32_t)i;
+                skey[p] = (uint16_t)k[u];
+            }
+        }
     }
     __syncthreads();
-    for (uint64_t i = lo + t; i < hi; i += blockDim.x) {
-        const uint32_t k = bucket_key(a, i);
-        order[base[kBucketKeys - 1 - k] + atomicAdd(&h[k], 1u)] = (uint32_t)i;
-    }
+    const uint32_t n = (uint32_t)(hi - lo);
+    for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
 }
 
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allow_pad, hipStream_t s) {
-    // work: histogram | fill counters | tile-queue head | tile count, zeroed
-    // here; order: bucket_words(count) - kBucketWork uint32.
-    // Rounded up to 16 B: one fill kernel instead of a body and a tail (the
-    // bytes past kBucketWork are `order` entries the scatter writes anyway).
-    (void)hipMemsetAsync(work, 0, (kBucketWork * sizeof(uint32_t) + 15) & ~(size_t)15, s);
-    uint64_t nb = (a.count + 1023) / 1024;
-    if (nb > kBucketBlocks) nb = kBucketBlocks;
-    const uint64_t chunk = (a.count + nb - 1) / nb;
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a, work);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)((a.count + chunk - 1) / chunk)), dim3(1024), 0, s, a,
-                       work, work + kBucketKeys, work + kBucketNTiles, order, chunk, allow_pad);
+    // work: [tot | spare | tile-queue head | entry count] then `order`
+    // (bucket_order_words), then cnt, base (nb x kBucketKeys each) and the
+    // 16-bit keys; every word the kernels read is written
+    // first by an earlier kernel of the three (no memset).
+    const uint64_t chunk = bucket_chunk(a.count);
+    const uint32_t nb = (uint32_t)bucket_blocks(a.count);
+    uint32_t* cnt = order + bucket_order_words(a.count);
+    uint32_t* base = cnt + (uint64_t)nb * kBucketKeys;
+    uint16_t* keys = reinterpret_cast<uint16_t*>(base + (uint64_t)nb * kBucketKeys);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, keys);
+    hipLaunchKernelGGL(bucket_base_kernel, dim3((kBucketKeys + 3) / 4), dim3(256), 0, s, cnt, nb, base, work);
+    hipLaunchKernelGGL(bucket_place_kernel, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys, work,
+                       order, allow_pad);
 }
 
 // ------------------------------------------------------------- dispatch

@@ -114,12 +114,16 @@ struct TileTrace {
 #define LCB_TRACE(...)
 #endif
 
+#ifndef LCB_FIXED_WAVES
+#define LCB_FIXED_WAVES 4
+#endif
+constexpr int kFixedWaves = LCB_FIXED_WAVES;   // waves (8 KiB slabs) per workgroup
 template <class H, bool kHmac, int kAux>
-__global__ __launch_bounds__(256) void md_fixed_lds_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+__global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    uint64_t wave_first = ((uint64_t)blockIdx.x * kFixedWaves + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
     LCB_TRACE(TileTrace tr; const uint64_t trw = wave_first / 64; const uint64_t trc = __builtin_amdgcn_s_memtime();
               tr.mark(0); tr.w[1] = tr.w[0]; tr.w[5] = trace_hwid(); tr.w[6] = a.fixed_len / 128;)
@@ -299,13 +303,14 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
         // LDS-DMA fast path: fixed-stride, 16-B aligned records of at least one
         // whole 128-B line.
         if (fixed_stride_lines(a)) {
-            const dim3 grid((unsigned)((a.count + 255) / 256));
+            constexpr unsigned T = 64 * kFixedWaves;
+            const dim3 grid((unsigned)((a.count + T - 1) / T));
             if (a.stride % 128 == 0 && reinterpret_cast<uintptr_t>(a.data) % 128 == 0) {
-                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kLdsAux>), grid, dim3(256), 0, s, a);
-                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kLdsAux>), grid, dim3(256), 0, s, a);
+                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kLdsAux>), grid, dim3(T), 0, s, a);
+                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kLdsAux>), grid, dim3(T), 0, s, a);
             } else {
-                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kGatherAux>), grid, dim3(256), 0, s, a);
-                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kGatherAux>), grid, dim3(256), 0, s, a);
+                if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kGatherAux>), grid, dim3(T), 0, s, a);
+                else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kGatherAux>), grid, dim3(T), 0, s, a);
             }
             return;
         }

@@ -73,10 +73,13 @@ def main():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-layouts", action="store_true", help="skip the MD5 layout / 1 KiB rows")
     ap.add_argument("--c4-algs", default="", help="C4 passes of these algorithms (full steps each)")
+    ap.add_argument("--no-packets", action="store_true", help="skip the ragged_packets rows")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     bench.settle()
-    print(json.dumps({"ragged_packets": bench.bench_packets(10, a.steps, tuple(a.algs.split(",")))}), flush=True)
+    if not a.no_packets:
+        print(json.dumps({"ragged_packets": bench.bench_packets(10, a.steps, tuple(a.algs.split(",")))}),
+              flush=True)
     if not a.no_layouts:
         for kind in ("sorted", "aligned128"):
             print(json.dumps(packets_layout(kind, a.steps)), flush=True)

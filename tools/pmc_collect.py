@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Turn one GPU session's rocprofv3 --pmc passes (tools/pmc_session.sh) into
+the committed counter files bench.py reads, each stamped with the machine
+code of the kernel it describes (tools/codestamp.py):
+
+  profiles/pmc_<alg>.json   HBM bytes per launch of each algorithm's kernel on
+                            the bench workload (1M x 1 KiB, fixed stride):
+                            read = 2 x FETCH_SIZE (gfx950 wide-stream
+                            correction, MI355X_MICROARCH.md HBM section),
+                            write = WRITE_SIZE;
+  profiles/valu_counts.json SQ_INSTS_VALU per launch (the VALU floor);
+  profiles/pmc_tiles.json   the same counters for the ragged tile kernel on
+                            the packet and C4 workloads, against their
+                            algorithmic bytes.
+
+usage: pmc_collect.py <session dir> <round tag> [lib.so]"""
+import collections
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import codestamp  # noqa: E402
+
+CXXFILT = "c++filt"
+# The kernel each algorithm launches on the bench workload (1M x 1 KiB,
+# 128-B aligned stride: the nt line stream, aux 2).
+BENCH_KERNEL = {
+    "md5": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Md5, false, 2>",
+    "sha1": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha1, false, 2>",
+    "sha224": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha256<true>, false, 2>",
+    "sha256": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha256<false>, false, 2>",
+    "sha384": "lcbgpu::md_batch_kernel<lcbgpu::Sha512<true>, false, false>",
+    "sha512": "lcbgpu::md_batch_kernel<lcbgpu::Sha512<false>, false, false>",
+    "gost256": "lcbgpu::gost_plain2_kernel<true>",
+    "gost512": "lcbgpu::gost_plain2_kernel<false>",
+}
+DIGEST = {"md5": 16, "sha1": 20, "sha224": 28, "sha256": 32, "sha384": 48, "sha512": 64, "gost256": 32,
+          "gost512": 64}
+
+
+def demangled_symbols(so):
+    names = sorted(codestamp.kernel_stamps(so))
+    out = subprocess.run([CXXFILT], input="\n".join(names), capture_output=True, text=True, check=True).stdout
+    return {d.replace("void ", "").split("(")[0].strip(): m for m, d in zip(names, out.splitlines())}
+
+
+def passes(d, pattern):
+    """{kernel (demangled, no 'void ', no args): {counter: [values per dispatch]}} of the pmc dirs."""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, pattern, "run_counter_collection.csv"))):
+        for row in csv.DictReader(open(f)):
+            k = row["Kernel_Name"].replace("void ", "").split("(")[0].strip()
+            acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return acc
+
+
+def mean(v):
+    return sum(v) / len(v) if v else None
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    so = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so")
+    sym = demangled_symbols(so)
+    stamps = codestamp.kernel_stamps(so)
+
+    def stamp(demangled):
+        m = sym[demangled]
+        return {"kernel": demangled, "kernel_symbol": m, "code_sha256": stamps[m]}
+
+    prof = os.path.join(ROOT, "profiles")
+    fixed = passes(src, "kb_*")
+    valu = {}
+    for alg, k in BENCH_KERNEL.items():
+        c = fixed.get(k)
+        if not c or not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE"):
+            print("missing counters for", alg, k)
+            continue
+        rd = 2 * mean(c["FETCH_SIZE"]) * 1024
+        wr = mean(c["WRITE_SIZE"]) * 1024
+        alg_bytes = (1 << 20) * (1024 + DIGEST[alg])
+        rec = {"alg": alg, "count": 1 << 20, "msg_len": 1024, "round": tag}
+        rec.update(stamp(k))
+        rec.update({"FETCH_SIZE_KiB": mean(c["FETCH_SIZE"]), "WRITE_SIZE_KiB": mean(c["WRITE_SIZE"]),
+                    "dispatches": len(c["FETCH_SIZE"]),
+                    "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream under-count, MI355X_MICROARCH.md HBM "
+                                  "section); write = WRITE_SIZE",
+                    "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+                    "algorithmic_bytes": alg_bytes, "traffic_over_algorithmic": round((rd + wr) / alg_bytes, 4),
+                    "source": os.path.relpath(src, ROOT)})
+        json.dump(rec, open(os.path.join(prof, "pmc_%s.json" % alg), "w"), indent=1)
+        print(alg, "traffic/algorithmic %.4f" % ((rd + wr) / alg_bytes))
+        if c.get("SQ_INSTS_VALU") and c.get("SQ_WAVES"):
+            v = {"SQ_INSTS_VALU": mean(c["SQ_INSTS_VALU"]), "SQ_WAVES": mean(c["SQ_WAVES"])}
+            v["valu_per_wave"] = round(v["SQ_INSTS_VALU"] / v["SQ_WAVES"])
+            if c.get("GRBM_GUI_ACTIVE"):
+                v["GRBM_GUI_ACTIVE"] = mean(c["GRBM_GUI_ACTIVE"])
+            v.update(stamp(k))
+            valu[alg] = v
+    if valu:
+        json.dump({"what": "SQ_INSTS_VALU (wave-instructions) per launch of each algorithm's kernel on the bench "
+                           "workload (1M x 1 KiB, fixed stride), rocprofv3 --pmc, mean over dispatches",
+                   "model": "VALU floor = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz): the mixed-stream issue "
+                            "rate of DESIGN.md 5 at the MI355X max clock",
+                   "round": tag, "source": os.path.relpath(src, ROOT), "count": 1 << 20, "msg_len": 1024,
+                   "algs": valu}, open(os.path.join(prof, "valu_counts.json"), "w"), indent=1)
+        print("valu_counts", {a: v["valu_per_wave"] for a, v in valu.items()})
+    # The ragged tile kernel (plain MD5 mode) on the packet and C4 workloads.
+    tiles = {}
+    k = "lcbgpu::md_tiles_kernel<lcbgpu::Md5, 0>"
+    sys.path.insert(0, ROOT)
+    from tests.golden_util import mixed_lengths, packet_layout
+    _, plens, ptotal = packet_layout()
+    clens = mixed_lengths(0x6C62636861736821, 1 << 20)
+    work = {"packets": ("kt_pkt_*", int(ptotal), len(plens)), "c4": ("kt_c4_*", int(sum(clens)), len(clens))}
+    for name, (pat, total, n) in work.items():
+        c = passes(src, pat).get(k)
+        if not c or not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE"):
+            print("missing tile counters for", name)
+            continue
+        rd = 2 * mean(c["FETCH_SIZE"]) * 1024
+        wr = mean(c["WRITE_SIZE"]) * 1024
+        # read: every message byte + its offset and length + its `order` entry; write: its digest
+        alg_rd, alg_wr = total + 16 * n, 16 * n
+        tiles[name] = {"messages": n, "message_bytes": total, "FETCH_SIZE_KiB": mean(c["FETCH_SIZE"]),
+                       "WRITE_SIZE_KiB": mean(c["WRITE_SIZE"]), "dispatches": len(c["FETCH_SIZE"]),
+                       "hbm_read_bytes": rd, "hbm_write_bytes": wr,
+                       "algorithmic_read_bytes": alg_rd, "algorithmic_write_bytes": alg_wr,
+                       "read_over_algorithmic": round(rd / alg_rd, 4), "write_over_algorithmic": round(wr / alg_wr, 4)}
+        print("tiles", name, "read/alg %.4f write/alg %.4f" % (rd / alg_rd, wr / alg_wr))
+    if tiles:
+        rec = {"round": tag, "source": os.path.relpath(src, ROOT),
+               "correction": "read = 2 x FETCH_SIZE, write = WRITE_SIZE (as pmc_<alg>.json)"}
+        rec.update(stamp(k))
+        rec["workloads"] = tiles
+        json.dump(rec, open(os.path.join(prof, "pmc_tiles.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
