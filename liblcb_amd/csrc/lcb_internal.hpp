@@ -19,7 +19,7 @@ struct KArgs {
     uint8_t* digests;          // packed count x D (CRC: count x uint32)
     const uint32_t* mid;       // HMAC mid-states (nullptr: plain digest)
     const uint32_t* init = nullptr;  // CRC: per-buffer X_update() value (nullptr: one-shot X())
-    uint32_t* tile_next = nullptr;   // bucketed batches: work-queue head of md_tiles_kernel (zeroed)
+    uint32_t* tile_next = nullptr;   // bucketed batches: [1] = entries of `order` (pads included), for md_tiles_kernel
     // Keyed batches (lcb_hash_batch_keyed): per-message key index into a key
     // table on the device; `mid` then holds 2 * kMidWords words per key.
     uint32_t key_mode = 0;           // kKeyNone / kKeyHmac / kKeyPrefix / kKeySuffix

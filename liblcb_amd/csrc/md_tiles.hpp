@@ -1,18 +1,15 @@
-// md_tiles.hpp — the persistent tile kernel of bucketed ragged MD-family
-// batches (the 64-byte-block hashes: MD5, SHA-1, SHA-224/256), included by
-// md_kernels.hpp.
+// md_tiles.hpp — the tile kernel of bucketed ragged MD-family batches (the
+// 64-byte-block hashes: MD5, SHA-1, SHA-224/256), included by md_kernels.hpp.
 //
 // A length-bucketed batch (lcb_kernels.hip launch_bucketing: `order` lists
 // messages by key = length class x start phase, longest class first, every
 // key's run padded to whole tiles for a large batch) is cut into TILES of 64
-// consecutive `order` entries; one wave hashes one tile at a time, lane =
-// message.  Workgroups of 4 waves (each wave owns an 8 KiB LDS slab), at
-// most kTileWgPerCu = 4 per CU: MD5 at 108-123 VGPRs runs 4 waves per SIMD
-// (H::kTileOcc), SHA-1 / SHA-224/256 at 156-194 VGPRs run 2 (they spill at
-// 3; being VALU-bound they lose nothing by it).  Every wave's first tile is
-// static (its global wave id), later ones come from a device-scope atomic
-// queue head; every wave leaves once the queue is past the last tile, so the
-// grid drains.
+// consecutive `order` entries; one wave hashes one tile, lane = message.
+// One-wave workgroups, one per tile, each with its 8 KiB LDS slab: the
+// hardware dispatcher hands out the tiles in order (longest first) and a
+// finished wave's slot takes the next tile at once.  MD5 at 108-123 VGPRs
+// runs 4 waves per SIMD (H::kTileOcc), SHA-1 / SHA-224/256 at 156-194 VGPRs
+// run 2 (they spill at 3; being VALU-bound they lose nothing by it).
 //
 // THE WHOLE-LINE STREAM.  The records of a tile share their length class
 // (their 64-B block counts differ by at most one) and the dword phase
@@ -61,8 +58,6 @@ namespace lcbgpu {
 
 enum { kTilePlain = 0, kTileHmac = 1, kTileKeyedHmac = 2, kTileKeyedSuffix = 3 };
 
-constexpr int kTileWaves = 4;     // waves per workgroup (one 8 KiB slab each)
-constexpr int kTileWgPerCu = 4;   // 4 waves per SIMD (kTileOcc): 128 KiB of LDS
 
 // __builtin_amdgcn_readfirstlane is 32-bit: a 64-bit value goes as two halves.
 __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
@@ -90,16 +85,6 @@ struct TileRec {
     bool valid;
 };
 
-// The next tile, claimed near the end of the current one in three steps, one
-// per stream line, so the dependent round trips (queue atomic -> order entry
-// -> offset / length) are waited for by the line stream's own waits.
-struct TileClaim {
-    uint64_t t;      // tile (wave-uniform)
-    uint32_t ent;    // this lane's order entry
-    TileRec r;
-    int stage;       // 0: nothing yet, 1: t, 2: ent, 3: r
-};
-
 __device__ __forceinline__ void tile_rec_load(const KArgs& a, uint32_t ent, TileRec& r) {
     r.valid = ent != kOrderPad;
     const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane(ent);
@@ -111,21 +96,6 @@ __device__ __forceinline__ void tile_rec_load(const KArgs& a, uint32_t ent, Tile
 __device__ __forceinline__ uint32_t tile_entry(const KArgs& a, uint64_t t, uint32_t lane, uint32_t norder) {
     const uint64_t i = t * 64 + lane;
     return i < norder ? gptr(a.order)[i] : kOrderPad;
-}
-
-// One step of the claim.  nwaves: first queue ticket = the static tiles.
-__device__ __forceinline__ void tile_claim_step(const KArgs& a, TileClaim& c, uint32_t lane, uint64_t ntiles,
-                                                uint32_t norder, uint32_t nwaves) {
-    if (c.stage == 0) {
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(a.tile_next, 1u);   // device scope, returns the old head
-        c.t = (uint64_t)nwaves + (uint32_t)__builtin_amdgcn_readfirstlane(v);
-    } else if (c.stage == 1) {
-        if (c.t < ntiles) c.ent = tile_entry(a, c.t, lane, norder);
-    } else if (c.stage == 2) {
-        if (c.t < ntiles) tile_rec_load(a, c.ent, c.r);
-    }
-    ++c.stage;
 }
 
 // Message geometry / key of a lane for the tile modes.
@@ -187,20 +157,28 @@ __device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint6
     if (b >= nblk) return;         // this lane is done (or has no block here: b = -1)
     const uint64_t pos = (uint64_t)b * 64;
     if (pos + 64 > len) {          // the block holds the end of the message
-        const int rb = pos >= len ? 0 : (int)(len - pos);   // message bytes in the block
+        const uint32_t rb = pos >= len ? 0u : (uint32_t)(len - pos);   // message bytes in the block
+        // Words below the end word e are message words, words above it
+        // zero; word e keeps its rb & 3 message bytes and takes the 0x80
+        // terminator after them when the message (m.total == len: every mode
+        // but the keyed suffix, whose tail is not assembled here) ends in
+        // this block: 5 VALU per word (was 10, with put_byte's pass).
+        const uint32_t e = rb >> 2, sb = 8u * (rb & 3u);
+        const uint32_t pm = (1u << sb) - 1u;
+        const uint32_t pb = (m.total == len && len >= pos) ? (0x80u << sb) : 0u;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int v = rb - 4 * k;
-            w[k] &= v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu >> (32 - 8 * v)));
+            const uint32_t part = (w[k] & pm) | pb;
+            w[k] = e > (uint32_t)k ? w[k] : (e == (uint32_t)k ? part : 0u);
         }
-        if (m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
+        if (m.total != len && m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
         if (b + 1 == nblk) H::put_length(w, m.total + m.prefix);
     }
     tile_compress(st, w);
 }
 
-// Initial state, materialised inside the tile loop: as plain constants the
-// compiler hoists them out of the persistent loop and spills them.
+// Initial state, materialised where the line loop starts (as plain
+// constants they were hoisted and held in registers across the loop).
 template <class H>
 __device__ __forceinline__ void tile_init(H& st) {
     if constexpr (std::is_same<H, Md5>::value) {
@@ -214,8 +192,8 @@ __device__ __forceinline__ void tile_init(H& st) {
 }
 
 // The HMAC mid-state pointer re-defined per use: its words (wave-uniform
-// for one key) are loaded per tile instead of being hoisted out of the
-// persistent loop into 8 SGPRs held all along (which spilled SGPRs).
+// for one key) are loaded where needed instead of being hoisted into 8
+// SGPRs held across the line loop.
 __device__ __forceinline__ const uint32_t* tile_mid(const KArgs& a) {
     const uint32_t* mid = a.mid;
     asm volatile("" : "+s"(mid));
@@ -402,8 +380,7 @@ struct TileGatherStream {
 };
 
 template <class H, int kMode, int kR>
-__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
-                                               TileClaim& cl, uint64_t ntiles, uint32_t norder, uint32_t nwaves
+__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab
                                                LCB_TRACE(, TileTrace& tr)) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
     const uint32_t sh = p32 & 3u;
@@ -456,7 +433,6 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         if (L >= NS) ls.issue_masked(L, lastc, rot());
         else ls.issue(L);
     };
-    const uint32_t c0 = NL > 3 ? NL - 3 : 0u;                // first claim step
     // Keyed suffix: the stream ends with the whole-block lines, the rest
     // (under two lines of message, the key) goes through the per-lane loop:
     // the key's window assembly next to a streamed line needs more VGPRs
@@ -472,7 +448,6 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         ls.take(y);
         LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
         if (L + 1 < LE) issue(L + 1);
-        if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         uint32_t w[16];
         if (L > 0) {   // block 2L - 1 - h: the carry merged with this line's wrapped chunks
             if (rotated) tile_merge(c, y, rot());
@@ -487,7 +462,6 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     if constexpr (kMode == kTileKeyedSuffix) {
         const uint32_t nd = LF ? 2u * LF - 1u - half() : 0u;       // blocks 0 .. nd - 1 done
         const uint64_t done = (uint64_t)nd * 64u;
-        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         md_message2(st, r.p + done, len - done, m_.K, m_.kl, m_.prefix + done);
         tile_finish<H, kMode>(a, st, r);
         return;
@@ -501,7 +475,6 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             ls.take(y);
             LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
             if (L + 1 < NL) issue(L + 1);
-            if (L >= c0 && cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
         } else {
 #pragma unroll
             for (int k = 0; k < 32; ++k) y[k] = 0u;
@@ -522,47 +495,44 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     tile_finish<H, kMode>(a, st, r);
 }
 
+// One tile per wave: the hardware dispatcher hands the tiles out in
+// blockIdx order (longest class first), one-wave workgroups (8 KiB of LDS
+// each, so a finished wave's slot is free at once).  A persistent grid with
+// a tile queue (round 3) ran 4-15 % slower: its waves keep their age for
+// the whole kernel and the SIMD's arbiter favours the oldest, so the
+// youngest wave of a SIMD ran 2.5x slower per line than the oldest and
+// the kernel ended with the starved waves' tiles (tools/tile_trace.py;
+// profiles/r4_tile_np_ab.txt).
 template <class H, int kMode>
-__global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(KArgs a, uint32_t nwaves) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kTileWaves][8192];
-    // Wave index as a scalar: the slab base (every DMA's M0) stays in SGPRs.
-    const uint32_t lane = threadIdx.x & 63, wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[8192];
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
     const uint64_t ntiles = (norder + 63) / 64;
-    TileClaim cl;
-    cl.t = (uint64_t)blockIdx.x * kTileWaves + wv;   // first tile: static
-    cl.stage = 3;
-    if (cl.t < ntiles) tile_rec_load(a, tile_entry(a, cl.t, lane, norder), cl.r);
-    while (cl.t < ntiles) {
-        const TileRec r = cl.r;
-        LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0; const uint64_t trt = cl.t;
-                  const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
-        cl.stage = 0;
-        // The lane id re-defined per tile: what the tile derives from it
-        // (bpermute addresses, slab slots, chunk numbers) is formed per tile
-        // instead of being hoisted out of the loop into VGPRs held all along.
-        uint32_t lane = threadIdx.x & 63;
-        asm volatile("" : "+v"(lane));
-        // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
-        const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
-        const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
-        if (__all(Rl == R)) {
-            // One copy of the line loop per dword phase R: the block window's
-            // word selection is static (no per-call dispatch and the register
-            // moves that merge its cases).
-            switch (R) {
-            case 0: md_tile_stream<H, kMode, 0>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
-            case 1: md_tile_stream<H, kMode, 1>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
-            case 2: md_tile_stream<H, kMode, 2>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
-            default: md_tile_stream<H, kMode, 3>(a, r, lane, &slab[wv][0], cl, ntiles, norder, nwaves LCB_TRACE(, tr)); break;
-            }
-        } else {
-            md_tile_direct<H, kMode>(a, r);
+    const uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;                   // the grid is an upper bound
+    TileRec r;
+    tile_rec_load(a, tile_entry(a, t, lane, norder), r);
+    LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0;
+              const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
+    // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
+    const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
+    const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
+    if (__all(Rl == R)) {
+        // One copy of the line loop per dword phase R: the block window's
+        // word selection is static (no per-call dispatch and the register
+        // moves that merge its cases).
+        switch (R) {
+        case 0: md_tile_stream<H, kMode, 0>(a, r, lane, slab LCB_TRACE(, tr)); break;
+        case 1: md_tile_stream<H, kMode, 1>(a, r, lane, slab LCB_TRACE(, tr)); break;
+        case 2: md_tile_stream<H, kMode, 2>(a, r, lane, slab LCB_TRACE(, tr)); break;
+        default: md_tile_stream<H, kMode, 3>(a, r, lane, slab LCB_TRACE(, tr)); break;
         }
-        LCB_TRACE(tr.mark(4); tr.w[6] |= ((uint64_t)blockIdx.x * kTileWaves + wv) << 16;
-                  tr.w[7] = __builtin_amdgcn_s_memtime() - trc; tr.put(g_tile_trace, trt, lane);)
-        while (cl.stage < 3) tile_claim_step(a, cl, lane, ntiles, norder, nwaves);
+    } else {
+        md_tile_direct<H, kMode>(a, r);
     }
+    LCB_TRACE(tr.mark(4); tr.w[6] |= t << 16; tr.w[7] = __builtin_amdgcn_s_memtime() - trc;
+              tr.put(g_tile_trace, t, lane);)
 }
 
 // Launch of the tile kernel on a bucketed batch (a.order, a.tile_next set);
@@ -570,18 +540,10 @@ __global__ __launch_bounds__(64 * kTileWaves, H::kTileOcc) void md_tiles_kernel(
 template <class H, int kMode>
 __host__ bool launch_tiles(const KArgs& a, hipStream_t s) {
     if constexpr (H::kTileOcc > 0) {
-        auto kern = md_tiles_kernel<H, kMode>;
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kTileWaves, 0) != hipSuccess || per_cu <= 0)
-            per_cu = 1;
-        per_cu = per_cu > kTileWgPerCu ? kTileWgPerCu : per_cu;
-        // Upper bound of the tile count (the device knows the exact one).
+        // One wave per tile; the tile count is known on the device only, so
+        // the grid is its upper bound (extra waves leave at once).
         const uint64_t ntiles = (a.count + 63) / 64 + kBucketKeys;
-        uint64_t grid = (uint64_t)per_cu * device_cu_count();
-        const uint64_t need = (ntiles + kTileWaves - 1) / kTileWaves;
-        if (grid > need) grid = need > 0 ? need : 1;
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * kTileWaves), 0, s, a,
-                           (uint32_t)(grid * kTileWaves));
+        hipLaunchKernelGGL((md_tiles_kernel<H, kMode>), dim3((unsigned)ntiles), dim3(64), 0, s, a);
         return true;
     } else {
         (void)a;

@@ -291,7 +291,7 @@ def test_bucketed_equals_unbucketed(gpu, oracle):
 @pytest.mark.parametrize("layout", ["aligned16", "packed", "mostly_aligned"])
 def test_ragged_line_stream(gpu, oracle, layout):
     """Bucketed ragged batches (count above the bucketing threshold) take the
-    persistent tile kernel (md_tiles_kernel): tiles whose records all start
+    tile kernel (md_tiles_kernel): tiles whose records all start
     16-B aligned with equal line counts stream their lines through LDS, the
     others load per lane.  Lengths 0..3000 plus a few 64 KiB records, so waves
     mix records with and without whole lines; plain and HMAC."""
