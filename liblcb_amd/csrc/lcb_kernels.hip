@@ -142,8 +142,7 @@ __device__ __forceinline__ uint32_t bucket_key(const KArgs& a, uint64_t i) {
 //                        order (one wave; runs padded to whole tiles for a
 //                        large batch) and places its messages at
 //                        start[k] + base[k][b] + rank (LDS atomics); block 0
-//                        writes the pad entries, the entry count and a zero
-//                        tile-queue head.
+//                        writes the pad entries and the entry count.
 // Messages per thread in one unrolled step of the bucketing kernels (their
 // loads issued together, not one round trip per message).
 constexpr int kBucketUnroll = 4;
@@ -220,11 +219,17 @@ __global__ __launch_bounds__(256) void bucket_base_kernel(const uint32_t* cnt, u
 // counts), then writes `order` in sorted order: consecutive threads write
 // consecutive entries of one key's run, so a wave's 64 stores cover a few
 // contiguous runs instead of 64 scattered dwords (each a partial-line write).
+// kTiles: the tile kernel's form -- runs padded to whole tiles (large
+// batches) and every entry written as its 16-B record (address, length,
+// index; KArgs::tile_recs), the offset and length gathered here once so
+// that a tile's start is one coalesced load instead of a dependent chain
+// (order -> offset/length: ~6 us per tile under load, tools/tile_trace.py).
 static_assert(kBucketChunkMax <= 8192, "a block's chunk sorts in LDS");
+template <bool kTiles>
 __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t chunk, uint32_t nb,
                                                             const uint32_t* cnt, const uint32_t* base,
                                                             const uint32_t* tot, const uint16_t* keys,
-                                                            uint32_t* work, uint32_t* order, bool allow_pad) {
+                                                            uint32_t* work, uint32_t* order) {
     __shared__ uint32_t h[kBucketKeys];        // run start in `order` of this block's entries, per key
     __shared__ uint32_t loc[kBucketKeys];      // local (sorted) offset per key, then the fill cursor
     __shared__ uint32_t len_s[kBucketKeys];
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     // scans the block's own counts (ascending: any order works locally).
     const uint32_t hk = t < (uint32_t)kBucketKeys ? gptr(tot)[t] : 0u;
     const int used = __syncthreads_count(hk != 0);
-    const bool pad = allow_pad && a.count >= kBucketPadRatio * 64 * (uint64_t)used;
+    const bool pad = kTiles && a.count >= kBucketPadRatio * 64 * (uint64_t)used;
     if (t < (uint32_t)kBucketKeys) len_s[t] = pad ? (hk + 63u) & ~63u : hk;
     __syncthreads();
     constexpr int kPer = (kBucketKeys + 63) / 64;
@@ -279,14 +284,14 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     if (t < (uint32_t)kBucketKeys) {
         const uint32_t start = h[t];
         if (blockIdx.x == 0)
-            for (uint32_t e = start + hk; e < start + len_s[t]; ++e) gptr(order)[e] = kOrderPad;
+            for (uint32_t e = start + hk; e < start + len_s[t]; ++e) {
+                if (kTiles) *reinterpret_cast<uint4*>(gptr(order) + 4ull * e) = make_uint4(0u, 0u, 0u, kOrderPad);
+                else gptr(order)[e] = kOrderPad;
+            }
         // order position of the key's first local entry, minus its local offset
         h[t] = start + gptr(base)[(uint64_t)t * nb + blockIdx.x] - loc[t];
     }
-    if (blockIdx.x == 0 && t == 0) {
-        gptr(work)[kBucketNTiles] = misc[0];
-        gptr(work)[kBucketHead] = 0u;            // tile-queue head
-    }
+    if (blockIdx.x == 0 && t == 0) gptr(work)[kBucketNTiles] = misc[0];
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
@@ -310,11 +315,21 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     }
     __syncthreads();
     const uint32_t n = (uint32_t)(hi - lo);
-    for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
+    if constexpr (kTiles) {
+        for (uint32_t p = t; p < n; p += blockDim.x) {
+            const uint32_t i = sidx[p];
+            const uint64_t ad = reinterpret_cast<uintptr_t>(a.data) +
+                                (a.offsets ? gptr(a.offsets)[i] : (uint64_t)i * a.stride);
+            *reinterpret_cast<uint4*>(gptr(order) + 4ull * (h[skey[p]] + p)) =
+                make_uint4((uint32_t)ad, (uint32_t)(ad >> 32), gptr(a.lengths)[i], i);
+        }
+    } else {
+        for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
+    }
 }
 
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allow_pad, hipStream_t s) {
-    // work: [tot | spare | tile-queue head | entry count] then `order`
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, hipStream_t s) {
+    // work: [tot | spare | spare | entry count] then `order`
     // (bucket_order_words), then cnt, base (nb x kBucketKeys each) and the
     // 16-bit keys; every word the kernels read is written
     // first by an earlier kernel of the three (no memset).
@@ -325,8 +340,12 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool allo
     uint16_t* keys = reinterpret_cast<uint16_t*>(base + (uint64_t)nb * kBucketKeys);
     hipLaunchKernelGGL(bucket_count_kernel, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, keys);
     hipLaunchKernelGGL(bucket_base_kernel, dim3((kBucketKeys + 3) / 4), dim3(256), 0, s, cnt, nb, base, work);
-    hipLaunchKernelGGL(bucket_place_kernel, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys, work,
-                       order, allow_pad);
+    if (tiles)
+        hipLaunchKernelGGL(bucket_place_kernel<true>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
+                           work, order);
+    else
+        hipLaunchKernelGGL(bucket_place_kernel<false>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
+                           work, order);
 }
 
 // ------------------------------------------------------------- dispatch

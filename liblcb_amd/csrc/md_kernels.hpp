@@ -124,17 +124,24 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint64_t wave_first = ((uint64_t)blockIdx.x * kFixedWaves + wv) * 64;
-    if (wave_first >= a.count) return;  // wave-uniform
+    // The arguments line 0's issue needs, loaded together (one scalar round
+    // trip; the compiler otherwise loads the count, branches, then loads the
+    // rest: two round trips before every wave's first line).
+    const uint8_t* data = a.data;
+    uint64_t count = a.count, stride = a.stride;
+    uint32_t fixed_len = a.fixed_len;
+    asm volatile("" : "+s"(data), "+s"(count), "+s"(stride), "+s"(fixed_len));
+    if (wave_first >= count) return;  // wave-uniform
     LCB_TRACE(TileTrace tr; const uint64_t trw = wave_first / 64; const uint64_t trc = __builtin_amdgcn_s_memtime();
-              tr.mark(0); tr.w[1] = tr.w[0]; tr.w[5] = trace_hwid(); tr.w[6] = a.fixed_len / 128;)
+              tr.mark(0); tr.w[1] = tr.w[0]; tr.w[5] = trace_hwid(); tr.w[6] = fixed_len / 128;)
     // A partial last wave moves back over its predecessor's records (count >=
     // 64, fixed_stride_lines) and stores only its own: no per-lane clamping.
-    const uint64_t last = a.count - 1;
+    const uint64_t last = count - 1;
     const uint32_t skip = wave_first + 63 > last ? (uint32_t)(wave_first + 63 - last) : 0u;
     wave_first -= skip;
-    const uint64_t nlines = a.fixed_len / 128;
+    const uint64_t nlines = fixed_len / 128;
     LdsStridedStream ls;
-    ls.init(a.data, a.stride, wave_first, lane, &slab[wv][0]);
+    ls.init(data, stride, wave_first, lane, &slab[wv][0]);
     H st;
     uint64_t prefix = 0;
     if (kHmac) {
@@ -158,8 +165,8 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     }
     if (lane < skip) return;
     const uint64_t i = wave_first + lane;
-    const uint8_t* msg = a.data + i * a.stride + nlines * 128;
-    const uint64_t tail = (uint64_t)a.fixed_len - nlines * 128;
+    const uint8_t* msg = data + i * stride + nlines * 128;
+    const uint64_t tail = (uint64_t)fixed_len - nlines * 128;
     if (tail == 0)  // wave-uniform: schedule of the pad block on the SALU
         md_pad_only(st, prefix + nlines * 128);
     else
@@ -315,7 +322,7 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
             return;
         }
     }
-    if (a.order && a.tile_next) {  // bucketed ragged batch: persistent tile queue
+    if (a.tile_recs) {  // bucketed ragged batch: the tile kernel
         if (hmac ? launch_tiles<H, kTileHmac>(a, s) : launch_tiles<H, kTilePlain>(a, s)) return;
     }
     if (a.count < kPfMaxCount) {
@@ -329,7 +336,7 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
 
 template <class H>
 void launch_md_keyed(const KArgs& a, hipStream_t s) {
-    if (a.order && a.tile_next) {  // bucketed ragged batch: the tile kernel's keyed modes
+    if (a.tile_recs) {  // bucketed ragged batch: the tile kernel's keyed modes
         if (a.key_mode == kKeyHmac && launch_tiles<H, kTileKeyedHmac>(a, s)) return;
         if (a.key_mode == kKeySuffix && launch_tiles<H, kTileKeyedSuffix>(a, s)) return;
     }

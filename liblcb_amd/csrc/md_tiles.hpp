@@ -75,9 +75,12 @@ __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     return k < a.nkeys ? k : a.nkeys - 1;
 }
 
-// One lane's record of a tile.  A pad entry (kOrderPad) takes lane 0's
-// record (never a pad) so every DMA address stays inside the batch; its
-// digest is not stored.
+// One lane's record of a tile: entry t * 64 + lane of the bucketing's tile
+// records (address, length, index; lcb_kernels.hip bucket_place_kernel),
+// one coalesced 1 KiB load per tile.  A pad entry (kOrderPad, or past the
+// last entry) takes lane 0's record (never a pad: a tile starts a key's run
+// or continues it) so every DMA address stays inside the batch; its digest
+// is not stored.
 struct TileRec {
     const uint8_t* p;
     uint32_t idx;
@@ -85,17 +88,18 @@ struct TileRec {
     bool valid;
 };
 
-__device__ __forceinline__ void tile_rec_load(const KArgs& a, uint32_t ent, TileRec& r) {
-    r.valid = ent != kOrderPad;
-    const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane(ent);
-    r.idx = r.valid ? ent : e0;
-    r.p = gptr(a.data) + (a.offsets ? gptr(a.offsets)[r.idx] : (uint64_t)r.idx * a.stride);
-    r.len = a.lengths ? gptr(a.lengths)[r.idx] : a.fixed_len;
-}
-
-__device__ __forceinline__ uint32_t tile_entry(const KArgs& a, uint64_t t, uint32_t lane, uint32_t norder) {
-    const uint64_t i = t * 64 + lane;
-    return i < norder ? gptr(a.order)[i] : kOrderPad;
+__device__ __forceinline__ void tile_rec_load(uint4 v, uint64_t i, uint32_t norder, TileRec& r) {
+    r.valid = i < norder && v.w != kOrderPad;
+    // Lane 0's record, read with every lane active (a readfirstlane inside
+    // the select would run under the pad lanes' EXEC and read a pad).
+    const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.x);
+    const uint32_t hi0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.y);
+    const uint32_t len0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.z);
+    const uint32_t idx0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.w);
+    const uint32_t lo = r.valid ? v.x : lo0, hi = r.valid ? v.y : hi0;
+    r.len = r.valid ? v.z : len0;
+    r.idx = r.valid ? v.w : idx0;
+    r.p = gptr(reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo));
 }
 
 // Message geometry / key of a lane for the tile modes.
@@ -399,16 +403,13 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // lines whose two blocks are whole message blocks (min), whole message
     // blocks (min).
     const uint64_t end = off + len;                          // record end, in stream bytes
-    const uint32_t nblk = (uint32_t)((m_.total + 8u) >> 6) + 1u;
-    const uint32_t nf = r.len >> 6;
-    const uint32_t NL = wave_max_u32((uint32_t)((end + 127u) >> 7)), NS = wave_min_u32((uint32_t)(end >> 7));
-    const uint32_t NB = wave_max_u32(nblk + h), NF = wave_min_u32(nf);
-    uint32_t LF = wave_min_u32((nf + h + 1u) >> 1);
-    if (LF > NL) LF = NL;
     // The tile's stream bases: 32-bit offsets from the lowest (saddr form)
     // when the tile spans less than 4 GiB, else the per-lane loop.  Bases
     // are compared as signed 128-B line deltas from lane 0's, so each bound
-    // is one 32-bit reduction.
+    // is one 32-bit reduction.  These three reductions come first: line 0
+    // is issued (masked: it is right for any record) before the rest of
+    // the geometry, whose reductions then run under its latency.
+    const uint32_t NL = wave_max_u32((uint32_t)((end + 127u) >> 7));
     const uint64_t base = (uint64_t)reinterpret_cast<uintptr_t>(r.p) - off;
     const uint64_t b0 = readfirstlane64(base);
     const int64_t d = (int64_t)(base - b0);
@@ -423,22 +424,32 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         return;
     }
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
+    TileGatherStream ls;
+    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(dl - dmin) * 128u, m, lane, slab);
+    // Keyed suffix: the stream ends with the whole-block lines, the rest
+    // (under two lines of message, the key) goes through the per-lane loop:
+    // the key's window assembly next to a streamed line needs more VGPRs
+    // than the occupancy leaves.  Its line count needs the whole geometry.
+    if (kMode != kTileKeyedSuffix) ls.issue_masked(0, lastc, rot());
+    // The rest of the geometry: lines wholly inside every record (min),
+    // blocks of the padded (virtual) message + h (max), lines whose two
+    // blocks are whole message blocks (min), whole message blocks (min).
+    const uint32_t nblk = (uint32_t)((m_.total + 8u) >> 6) + 1u;
+    const uint32_t nf = r.len >> 6;
+    const uint32_t NS = wave_min_u32((uint32_t)(end >> 7));
+    const uint32_t NB = wave_max_u32(nblk + h), NF = wave_min_u32(nf);
+    uint32_t LF = wave_min_u32((nf + h + 1u) >> 1);
+    if (LF > NL) LF = NL;
     LCB_TRACE(tr.mark(1); tr.w[6] = NL;)
     // No lane's chunks rotated (every start on a 64-B half line, as in C4):
     // the carry needs no merge (wave-uniform).
     const bool rotated = !__all(m == 0);
-    TileGatherStream ls;
-    ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(dl - dmin) * 128u, m, lane, slab);
     auto issue = [&](uint32_t L) {
         if (L >= NS) ls.issue_masked(L, lastc, rot());
         else ls.issue(L);
     };
-    // Keyed suffix: the stream ends with the whole-block lines, the rest
-    // (under two lines of message, the key) goes through the per-lane loop:
-    // the key's window assembly next to a streamed line needs more VGPRs
-    // than the occupancy leaves.
     const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
-    if (LE) issue(0);
+    if (kMode == kTileKeyedSuffix && LE) issue(0);
     uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
     // Whole-block lines: both blocks of line L (2L - 1 - h and 2L - h) are
     // whole message blocks of every lane.
@@ -507,12 +518,18 @@ template <class H, int kMode>
 __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[8192];
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t norder = a.tile_next[1];   // entries of `order` (pads included), from the bucketing
-    const uint64_t ntiles = (norder + 63) / 64;
     const uint64_t t = blockIdx.x;
+    // The entry count and the tile's records load together (the records
+    // cover the whole grid, bucket_entries): two round trips to the first
+    // line's issue instead of four (kernel argument, count, argument,
+    // records).  The asm keeps the record load above the exit branch.
+    uint4 v = gptr(reinterpret_cast<const uint4*>(a.tile_recs))[t * 64 + lane];
+    uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w), "+s"(norder));
+    const uint64_t ntiles = (norder + 63) / 64;
     if (t >= ntiles) return;                   // the grid is an upper bound
     TileRec r;
-    tile_rec_load(a, tile_entry(a, t, lane, norder), r);
+    tile_rec_load(v, t * 64 + lane, norder, r);
     LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0;
               const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
@@ -535,7 +552,7 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
               tr.put(g_tile_trace, t, lane);)
 }
 
-// Launch of the tile kernel on a bucketed batch (a.order, a.tile_next set);
+// Launch of the tile kernel on a bucketed batch (a.tile_recs, a.tile_next set);
 // false if this hash has no tile kernel.
 template <class H, int kMode>
 __host__ bool launch_tiles(const KArgs& a, hipStream_t s) {

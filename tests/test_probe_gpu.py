@@ -61,5 +61,8 @@ def test_probe_rejects_bad_shapes(L):
     assert L.lcb_hash_gpu_read_probe(0, p, 64, 1024, 100, q, s) == errno.EINVAL      # no whole line
     assert L.lcb_hash_gpu_read_probe(0, p + 8, 64, 1024, 1024, q, s) == errno.EINVAL  # misaligned
     assert L.lcb_hash_gpu_read_probe(1, p, 3, 5, 5, q, s) == errno.EINVAL            # not 16-B multiple
-    assert L.lcb_hash_gpu_read_probe(2, p, 64, 1024, 1024, q, s) == errno.EINVAL     # unknown mode
+    assert L.lcb_hash_gpu_read_probe(2, p, 0, 1024, 1024, q, s) == errno.EINVAL      # GOST LPS: no lanes
+    assert L.lcb_hash_gpu_read_probe(2, p, 64, 1024, 1024, 0, s) == errno.EINVAL      # GOST LPS: no sink
+    assert L.lcb_hash_gpu_read_probe(3, p, 64, 1024, 1024, q, s) == errno.EINVAL     # unknown mode
+    assert L.lcb_hash_gpu_read_probe(2, p, 64, 1024, 1024, q, s) == 0                # GOST LPS chain runs
     torch.cuda.synchronize()
