@@ -73,6 +73,11 @@ constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
 constexpr int kBucketHead = 2 * kBucketKeys;
 constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
 constexpr int kBucketWork = (2 * kBucketKeys + 2 + 3) & ~3;   // 16-B aligned permutation
+// A/B switch: the tile kernel's permutation as 16-B records (1) or as
+// message indices (0).
+#ifndef LCB_TILE_RECS
+#define LCB_TILE_RECS 0
+#endif
 // Messages per bucketing block: count / 1024, clamped to [4096, 8192] (the
 // placement sorts a block's whole chunk in LDS).
 constexpr uint64_t kBucketBlocksTarget = 1024;

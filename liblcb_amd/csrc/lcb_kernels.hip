@@ -285,7 +285,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
         const uint32_t start = h[t];
         if (blockIdx.x == 0)
             for (uint32_t e = start + hk; e < start + len_s[t]; ++e) {
-                if (kTiles) *reinterpret_cast<uint4*>(gptr(order) + 4ull * e) = make_uint4(0u, 0u, 0u, kOrderPad);
+                if (kTiles && LCB_TILE_RECS) *reinterpret_cast<uint4*>(gptr(order) + 4ull * e) = make_uint4(0u, 0u, 0u, kOrderPad);
                 else gptr(order)[e] = kOrderPad;
             }
         // order position of the key's first local entry, minus its local offset
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     }
     __syncthreads();
     const uint32_t n = (uint32_t)(hi - lo);
-    if constexpr (kTiles) {
+    if constexpr (kTiles && LCB_TILE_RECS) {
         for (uint32_t p = t; p < n; p += blockDim.x) {
             const uint32_t i = sidx[p];
             const uint64_t ad = reinterpret_cast<uintptr_t>(a.data) +

@@ -523,6 +523,7 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // cover the whole grid, bucket_entries): two round trips to the first
     // line's issue instead of four (kernel argument, count, argument,
     // records).  The asm keeps the record load above the exit branch.
+#if LCB_TILE_RECS
     uint4 v = gptr(reinterpret_cast<const uint4*>(a.tile_recs))[t * 64 + lane];
     uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w), "+s"(norder));
@@ -530,6 +531,19 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     if (t >= ntiles) return;                   // the grid is an upper bound
     TileRec r;
     tile_rec_load(v, t * 64 + lane, norder, r);
+#else
+    uint32_t ent = gptr(a.tile_recs)[t * 64 + lane];
+    uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
+    asm volatile("" : "+v"(ent), "+s"(norder));
+    const uint64_t ntiles = (norder + 63) / 64;
+    if (t >= ntiles) return;                   // the grid is an upper bound
+    TileRec r;
+    r.valid = t * 64 + lane < norder && ent != kOrderPad;
+    const uint32_t ent0 = (uint32_t)__builtin_amdgcn_readfirstlane(ent);
+    r.idx = r.valid ? ent : ent0;
+    r.p = gptr(a.data) + (a.offsets ? gptr(a.offsets)[r.idx] : (uint64_t)r.idx * a.stride);
+    r.len = a.lengths ? gptr(a.lengths)[r.idx] : a.fixed_len;
+#endif
     LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0;
               const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.

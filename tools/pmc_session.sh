@@ -8,7 +8,7 @@
 # profiles/pmc_*.json and valu_counts.json.  Each pass has its own limit; the
 # script stops at the first failure.   TAG=r4p bash tools/pmc_session.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r4p}
+TAG=${TAG:-r4a}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
@@ -18,6 +18,13 @@ for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
   timeout -s KILL 150 rocprofv3 --pmc $grp -d $O/kb_$i -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5,sha1,sha224,sha256,sha384,sha512,gost256,gost512 --reps 3 --warmup 3 > $O/kb_$i.log 2>&1
   rc=$?; echo "kb $i ($grp) rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
+# MD5 fixed-stride kernel only: wave occupancy and clock (SQ_WAVE_CYCLES /
+# SQ_BUSY_CYCLES), and why the dispatcher could not place a workgroup
+# (SPI resource-allocation stalls: LDS full, workgroup limit).
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS -d $O/kb_occ -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5 --reps 5 --warmup 5 > $O/kb_occ.log 2>&1
+rc=$?; echo "kb occ rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -s KILL 90 rocprofv3 --pmc SPI_RA_LDS_CU_FULL_CSN SPI_RA_TGLIM_CU_FULL_CSN -d $O/kb_spi -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5 --reps 5 --warmup 5 > $O/kb_spi.log 2>&1
+rc=$?; echo "kb spi rc=$rc"; [ $rc -ne 0 ] && exit $rc
 i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
