@@ -123,7 +123,7 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     // key: its length, the scan and the tile count must stay below 2^32.
     if (a.lengths && a.order == nullptr && a.count >= kBucketMaxCount) return EINVAL;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
-        // work: [key totals | spare | entry count | permutation | ...]
+        // work: [key totals | spare | spare | entry count | order | ...]
         const size_t bytes = bucket_words(a.count) * sizeof(uint32_t);
         if (work_buf) {
             work = work_buf;
@@ -132,9 +132,8 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
         }
         const bool tiles = tiles_take(alg, a);
         launch_bucketing(a, work, work + kBucketWork, tiles, s);
-        a.tile_next = work + kBucketHead;
-        if (tiles) a.tile_recs = work + kBucketWork;
-        else a.order = work + kBucketWork;
+        a.order = work + kBucketWork;
+        if (tiles) a.tile_next = work + kBucketHead;
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();

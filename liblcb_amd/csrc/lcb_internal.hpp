@@ -19,11 +19,9 @@ struct KArgs {
     uint8_t* digests;          // packed count x D (CRC: count x uint32)
     const uint32_t* mid;       // HMAC mid-states (nullptr: plain digest)
     const uint32_t* init = nullptr;  // CRC: per-buffer X_update() value (nullptr: one-shot X())
-    uint32_t* tile_next = nullptr;   // bucketed batches: [1] = entries of the permutation (pads included)
-    // Bucketed batches for the tile kernel: the permutation as 16-B records
-    // (address low, high, length, index or kOrderPad), so a tile's 64
-    // records arrive with one coalesced load (no order -> offset chain).
-    const uint32_t* tile_recs = nullptr;
+    // Bucketed batches for the tile kernel (set with a padded `order`):
+    // [1] = entries of `order`, pads included.
+    uint32_t* tile_next = nullptr;
     // Keyed batches (lcb_hash_batch_keyed): per-message key index into a key
     // table on the device; `mid` then holds 2 * kMidWords words per key.
     uint32_t key_mode = 0;           // kKeyNone / kKeyHmac / kKeyPrefix / kKeySuffix
@@ -66,18 +64,13 @@ constexpr int kBucketClasses = 122;
 constexpr int kBucketPhases = 4;
 constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
 // Bucketing scratch ahead of the permutation: per-key totals, a spare
-// block, the tile-queue head, the number of `order` entries (uint32 words).
+// block, a spare word, the number of `order` entries (uint32 words).
 // After the permutation: the per-block key counts, their per-block bases
 // (bucket_blocks(count) x kBucketKeys words each) and one 16-bit key per
 // message.
 constexpr int kBucketHead = 2 * kBucketKeys;
 constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
-constexpr int kBucketWork = (2 * kBucketKeys + 2 + 3) & ~3;   // 16-B aligned permutation
-// A/B switch: the tile kernel's permutation as 16-B records (1) or as
-// message indices (0).
-#ifndef LCB_TILE_RECS
-#define LCB_TILE_RECS 0
-#endif
+constexpr int kBucketWork = 2 * kBucketKeys + 2;
 // Messages per bucketing block: count / 1024, clamped to [4096, 8192] (the
 // placement sorts a block's whole chunk in LDS).
 constexpr uint64_t kBucketBlocksTarget = 1024;
@@ -97,14 +90,11 @@ constexpr uint32_t kOrderPad = 0xffffffffu;
 constexpr uint64_t kBucketPadRatio = 16;
 // Largest ragged batch the uint32 permutation can describe, pads included.
 constexpr uint64_t kBucketMaxCount = 0xffffffffull - 63ull * kBucketKeys;
-// Entries of the permutation, pads included, and the uint32 words it takes:
-// room for the tile kernel's 4-word records (the other kernels' `order`
-// uses the first quarter).
-// (The records cover the tile kernel's whole grid, (count + 63) / 64 +
-// kBucketKeys tiles of 64: it loads a tile's records before it knows the
-// entry count, and masks the entries past it.)
-inline size_t bucket_entries(uint64_t count) { return (size_t)count + 64ull * (kBucketKeys + 1); }
-inline size_t bucket_order_words(uint64_t count) { return 4 * bucket_entries(count); }
+// Words of `order`: the entries (count + at most 63 pads per key), rounded
+// up to the tile kernel's whole grid, (count + 63) / 64 + kBucketKeys tiles
+// of 64 -- it loads a tile's entries before it knows the entry count and
+// ignores those past it.
+inline size_t bucket_order_words(uint64_t count) { return (size_t)count + 64ull * (kBucketKeys + 1); }
 // uint32 words of bucketing scratch for a batch of `count` messages:
 // [work | permutation | per-block counts | per-block bases | 16-bit keys].
 inline size_t bucket_words(uint64_t count) {
@@ -163,14 +153,12 @@ void launch_chacha(const ChaArgs& a, uint64_t nparts, uint64_t* parts, uint64_t*
 void launch_crc(int variant, const KArgs& a, hipStream_t s);
 void crc_table_host(int variant, uint32_t* out);
 // Bucketing permutation of the ragged batch `a` (reads data/offsets/stride/
-// lengths/count) into `order` (bucket_words(count) - kBucketWork words);
-// `work` = kBucketWork words (key totals, entry count).  tiles: the tile
-// kernel's form -- each key's run padded to whole tiles when the batch is
-// large, 4-word records (KArgs::tile_recs); else one index per entry.
+// lengths/count) into `order` (bucket_order_words(count) words); `work` =
+// kBucketWork words (key totals, entry count).  tiles: the tile kernel's
+// form, each key's run padded to whole tiles when the batch is large.
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, hipStream_t s);
 // True when launch_batch(alg, a) runs the tile kernel on a bucketed batch:
-// only then is the permutation padded and written as tile records (every
-// other kernel reads `order` per lane).
+// only then may `order` hold pad entries (every other kernel reads it per lane).
 bool tiles_take(int alg, const KArgs& a);
 void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t key_len,
                       uint32_t* mid, hipStream_t s);

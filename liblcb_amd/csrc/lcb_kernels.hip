@@ -219,11 +219,8 @@ __global__ __launch_bounds__(256) void bucket_base_kernel(const uint32_t* cnt, u
 // counts), then writes `order` in sorted order: consecutive threads write
 // consecutive entries of one key's run, so a wave's 64 stores cover a few
 // contiguous runs instead of 64 scattered dwords (each a partial-line write).
-// kTiles: the tile kernel's form -- runs padded to whole tiles (large
-// batches) and every entry written as its 16-B record (address, length,
-// index; KArgs::tile_recs), the offset and length gathered here once so
-// that a tile's start is one coalesced load instead of a dependent chain
-// (order -> offset/length: ~6 us per tile under load, tools/tile_trace.py).
+// kTiles: the tile kernel's form, runs padded to whole tiles (large
+// batches).
 static_assert(kBucketChunkMax <= 8192, "a block's chunk sorts in LDS");
 template <bool kTiles>
 __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t chunk, uint32_t nb,
@@ -284,10 +281,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     if (t < (uint32_t)kBucketKeys) {
         const uint32_t start = h[t];
         if (blockIdx.x == 0)
-            for (uint32_t e = start + hk; e < start + len_s[t]; ++e) {
-                if (kTiles && LCB_TILE_RECS) *reinterpret_cast<uint4*>(gptr(order) + 4ull * e) = make_uint4(0u, 0u, 0u, kOrderPad);
-                else gptr(order)[e] = kOrderPad;
-            }
+            for (uint32_t e = start + hk; e < start + len_s[t]; ++e) gptr(order)[e] = kOrderPad;
         // order position of the key's first local entry, minus its local offset
         h[t] = start + gptr(base)[(uint64_t)t * nb + blockIdx.x] - loc[t];
     }
@@ -315,17 +309,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     }
     __syncthreads();
     const uint32_t n = (uint32_t)(hi - lo);
-    if constexpr (kTiles && LCB_TILE_RECS) {
-        for (uint32_t p = t; p < n; p += blockDim.x) {
-            const uint32_t i = sidx[p];
-            const uint64_t ad = reinterpret_cast<uintptr_t>(a.data) +
-                                (a.offsets ? gptr(a.offsets)[i] : (uint64_t)i * a.stride);
-            *reinterpret_cast<uint4*>(gptr(order) + 4ull * (h[skey[p]] + p)) =
-                make_uint4((uint32_t)ad, (uint32_t)(ad >> 32), gptr(a.lengths)[i], i);
-        }
-    } else {
-        for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
-    }
+    for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
 }
 
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, hipStream_t s) {

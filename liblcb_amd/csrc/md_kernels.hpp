@@ -322,7 +322,7 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
             return;
         }
     }
-    if (a.tile_recs) {  // bucketed ragged batch: the tile kernel
+    if (a.order && a.tile_next) {  // bucketed ragged batch: the tile kernel
         if (hmac ? launch_tiles<H, kTileHmac>(a, s) : launch_tiles<H, kTilePlain>(a, s)) return;
     }
     if (a.count < kPfMaxCount) {
@@ -336,7 +336,7 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
 
 template <class H>
 void launch_md_keyed(const KArgs& a, hipStream_t s) {
-    if (a.tile_recs) {  // bucketed ragged batch: the tile kernel's keyed modes
+    if (a.order && a.tile_next) {  // bucketed ragged batch: the tile kernel's keyed modes
         if (a.key_mode == kKeyHmac && launch_tiles<H, kTileKeyedHmac>(a, s)) return;
         if (a.key_mode == kKeySuffix && launch_tiles<H, kTileKeyedSuffix>(a, s)) return;
     }

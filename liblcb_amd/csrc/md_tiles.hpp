@@ -75,32 +75,16 @@ __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     return k < a.nkeys ? k : a.nkeys - 1;
 }
 
-// One lane's record of a tile: entry t * 64 + lane of the bucketing's tile
-// records (address, length, index; lcb_kernels.hip bucket_place_kernel),
-// one coalesced 1 KiB load per tile.  A pad entry (kOrderPad, or past the
-// last entry) takes lane 0's record (never a pad: a tile starts a key's run
-// or continues it) so every DMA address stays inside the batch; its digest
-// is not stored.
+// One lane's record of a tile.  A pad entry (kOrderPad, or past the last
+// entry) takes lane 0's record (never a pad: a tile starts a key's run or
+// continues it) so every DMA address stays inside the batch; its digest is
+// not stored.
 struct TileRec {
     const uint8_t* p;
     uint32_t idx;
     uint32_t len;
     bool valid;
 };
-
-__device__ __forceinline__ void tile_rec_load(uint4 v, uint64_t i, uint32_t norder, TileRec& r) {
-    r.valid = i < norder && v.w != kOrderPad;
-    // Lane 0's record, read with every lane active (a readfirstlane inside
-    // the select would run under the pad lanes' EXEC and read a pad).
-    const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.x);
-    const uint32_t hi0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.y);
-    const uint32_t len0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.z);
-    const uint32_t idx0 = (uint32_t)__builtin_amdgcn_readfirstlane(v.w);
-    const uint32_t lo = r.valid ? v.x : lo0, hi = r.valid ? v.y : hi0;
-    r.len = r.valid ? v.z : len0;
-    r.idx = r.valid ? v.w : idx0;
-    r.p = gptr(reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo));
-}
 
 // Message geometry / key of a lane for the tile modes.
 template <class H, int kMode>
@@ -519,31 +503,25 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[8192];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t t = blockIdx.x;
-    // The entry count and the tile's records load together (the records
-    // cover the whole grid, bucket_entries): two round trips to the first
-    // line's issue instead of four (kernel argument, count, argument,
-    // records).  The asm keeps the record load above the exit branch.
-#if LCB_TILE_RECS
-    uint4 v = gptr(reinterpret_cast<const uint4*>(a.tile_recs))[t * 64 + lane];
-    uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
-    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w), "+s"(norder));
-    const uint64_t ntiles = (norder + 63) / 64;
-    if (t >= ntiles) return;                   // the grid is an upper bound
-    TileRec r;
-    tile_rec_load(v, t * 64 + lane, norder, r);
-#else
-    uint32_t ent = gptr(a.tile_recs)[t * 64 + lane];
+    // The entry count and the tile's `order` entries load together (`order`
+    // covers the whole grid, bucket_order_words): three round trips to the
+    // first line's issue (kernel arguments, entries, offsets and lengths)
+    // instead of five.  The asm keeps the entry load above the exit branch.
+    // (16-B records written by the bucketing -- address, length, index --
+    // save one more round trip but cost the bucketing a gather and 12 B
+    // more per entry: 2 % slower on the packets, profiles/r4_tile_rec_ab.txt.)
+    uint32_t ent = gptr(a.order)[t * 64 + lane];
     uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
     asm volatile("" : "+v"(ent), "+s"(norder));
     const uint64_t ntiles = (norder + 63) / 64;
     if (t >= ntiles) return;                   // the grid is an upper bound
     TileRec r;
     r.valid = t * 64 + lane < norder && ent != kOrderPad;
+    // lane 0's entry, read with every lane active (never a pad: t < ntiles)
     const uint32_t ent0 = (uint32_t)__builtin_amdgcn_readfirstlane(ent);
     r.idx = r.valid ? ent : ent0;
     r.p = gptr(a.data) + (a.offsets ? gptr(a.offsets)[r.idx] : (uint64_t)r.idx * a.stride);
     r.len = a.lengths ? gptr(a.lengths)[r.idx] : a.fixed_len;
-#endif
     LCB_TRACE(TileTrace tr; tr.w[1] = tr.w[2] = tr.w[3] = 0; tr.w[6] = 0;
               const uint64_t trc = __builtin_amdgcn_s_memtime(); tr.mark(0); tr.w[5] = trace_hwid();)
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
@@ -566,7 +544,7 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
               tr.put(g_tile_trace, t, lane);)
 }
 
-// Launch of the tile kernel on a bucketed batch (a.tile_recs, a.tile_next set);
+// Launch of the tile kernel on a bucketed batch (a.order, a.tile_next set);
 // false if this hash has no tile kernel.
 template <class H, int kMode>
 __host__ bool launch_tiles(const KArgs& a, hipStream_t s) {

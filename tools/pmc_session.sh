@@ -25,6 +25,8 @@ timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_AC
 rc=$?; echo "kb occ rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 90 rocprofv3 --pmc SPI_RA_LDS_CU_FULL_CSN SPI_RA_TGLIM_CU_FULL_CSN -d $O/kb_spi -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5 --reps 5 --warmup 5 > $O/kb_spi.log 2>&1
 rc=$?; echo "kb spi rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VALU -d $O/kt_pktocc -o run --output-format csv -- python3 $R/tools/pkt_bench.py --steps 3 --no-layouts --no-c4 > $O/kt_pktocc.log 2>&1
+rc=$?; echo "kt pkt occ rc=$rc"; [ $rc -ne 0 ] && exit $rc
 i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
