@@ -249,6 +249,19 @@ def valu_floor_ms(alg, count):
     return n * VALU_CYCLES / (VALU_SIMDS * VALU_CLOCK_HZ) * 1e3
 
 
+def pmc_clock_ghz(alg):
+    """Median engine clock the PMC occupancy pass measured under this
+    algorithm's kernel (profiles/valu_counts.json `occupancy`, SQ_CYCLES per
+    engine / dispatch time), None when absent or stale."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "valu_counts.json")))["algs"][ALG_NAMES[alg]]
+        if not counters_current(rec):
+            return None
+        return float(rec["occupancy"]["clock_GHz_median"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def read_probes(data, count, steps=50, warmup=20):
     """Achievable HBM read rate on this box, GB/s: the digest
     kernels' own LDS-DMA line stream over the same records without the
@@ -795,6 +808,14 @@ def main():
                      "valu_floor_ms": round(vfloor, 4) if vfloor else None,
                      "valu_frac": round(vfloor / kms, 4) if vfloor else None},
     }
+    clk = pmc_clock_ghz(alg)
+    if vfloor and clk:
+        # The same VALU floor at the clock the kernel actually runs at (the
+        # 2.4 GHz of valu_floor_ms is the spec maximum; the power manager
+        # holds MD5 near 2.1).
+        f = vfloor * VALU_CLOCK_HZ / (clk * 1e9)
+        out["roofline"].update({"pmc_clock_GHz": clk, "valu_floor_ms_pmc_clock": round(f, 4),
+                                "valu_frac_pmc_clock": round(f / kms, 4)})
 
     if rank == 0 and world == 1 and not a.no_extras:
         # Achievable read rate on this box next to the spec peak: the same

@@ -295,6 +295,9 @@ __device__ __forceinline__ uint32_t group8_or(uint32_t v) {
 // Which chunks are valid comes from one word per group per line: every
 // lane's count of valid chunks in the line, 4 bits each, OR-reduced in the
 // group; the group's rotations travel the same way, 2 bits each, once.
+#ifndef LCB_TILE_SKIP
+#define LCB_TILE_SKIP 0
+#endif
 struct TileGatherStream {
     uint8_t* slab;
     uint32_t lane;
@@ -343,10 +346,20 @@ struct TileGatherStream {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             const uint32_t k = (((ln & 7u) ^ (uint32_t)g) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
+#if LCB_TILE_SKIP
+            // A chunk past its record's last byte is not loaded at all (the
+            // lane is off for that DMA; its slab slot keeps stale bytes, which
+            // lie past the message end and are masked).
+            if (k < ((nv >> (4 * g)) & 15u))
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + voff[g] + L * 128u),
+                                                 (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                                 kLdsAux);
+#else
             const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                              (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
                                              kLdsAux);
+#endif
         }
     }
     // Waits for the issued line, copies this lane's 128 B (raw LE words, the
@@ -366,6 +379,23 @@ struct TileGatherStream {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 };
+
+#ifndef LCB_TILE_PRIO
+#define LCB_TILE_PRIO 1
+#endif
+// Wave priority by remaining lines, longest remaining first (set every 16
+// lines; tiles under 128 lines stay at 0).  Among a SIMD's waves the arbiter
+// otherwise favours the oldest, so of two long tiles the younger, with more
+// left to do, ends last: in C4 the first round of 64 KiB tiles ended between
+// 1.1 and 2.9 ms, the second round's last tiles ran alone for the last
+// 0.8 ms (tools/tile_trace.py).  C4 4.54 -> 4.35 ms, packets and 1 KiB
+// records unchanged (profiles/r4_tile_prio_ab.txt).
+__device__ __forceinline__ void tile_prio(uint32_t left) {
+    if (left >= 384) __builtin_amdgcn_s_setprio(3);
+    else if (left >= 256) __builtin_amdgcn_s_setprio(2);
+    else if (left >= 128) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 
 template <class H, int kMode, int kR>
 __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab
@@ -440,6 +470,9 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     uint32_t L = 0;
     for (; L < LF; ++L) {
         uint32_t y[32];
+#if LCB_TILE_PRIO
+        if ((L & 15u) == 0) tile_prio(NL - L);
+#endif
         ls.take(y);
         LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
         if (L + 1 < LE) issue(L + 1);

@@ -63,6 +63,43 @@ def mean(v):
     return sum(v) / len(v) if v else None
 
 
+def median(v):
+    v = sorted(v)
+    return v[len(v) // 2] if v else None
+
+
+def occupancy(d, pattern, kernel, n_sq=32):
+    """Clock and issue statistics of `kernel` from an occupancy pass
+    (SQ_CYCLES, SQ_BUSY_CYCLES, SQ_WAVE_CYCLES, SQ_ACTIVE_INST_VALU), per
+    dispatch, medians: SQ_* counters are summed over the n_sq shader engines
+    (8 XCDs x 4); SQ_WAVE_CYCLES counts in units of 4 cycles; clock =
+    SQ_CYCLES / n_sq / dispatch duration."""
+    per = collections.defaultdict(dict)
+    for f in sorted(glob.glob(os.path.join(d, pattern, "run_counter_collection.csv"))):
+        for row in csv.DictReader(open(f)):
+            if row["Kernel_Name"].replace("void ", "").split("(")[0].strip() != kernel:
+                continue
+            dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+            per[row["Dispatch_Id"]][row["Counter_Name"]] = float(row["Counter_Value"])
+            per[row["Dispatch_Id"]]["dur_ns"] = dur
+    clk, wav, util, durs = [], [], [], []
+    for c in per.values():
+        if not all(k in c for k in ("SQ_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU")):
+            continue
+        clk.append(c["SQ_CYCLES"] / n_sq / c["dur_ns"])
+        wav.append(c["SQ_WAVE_CYCLES"] * 4 / c["SQ_BUSY_CYCLES"] / 8)          # 8 CUs per engine
+        util.append(c["SQ_ACTIVE_INST_VALU"] * 4 / (c["SQ_BUSY_CYCLES"] / n_sq * 1024))
+        durs.append(c["dur_ns"] / 1e6)
+    if not clk:
+        return None
+    return {"dispatches": len(clk), "clock_GHz_median": round(median(clk), 3),
+            "clock_GHz_range": [round(min(clk), 3), round(max(clk), 3)],
+            "waves_per_CU_median": round(median(wav), 2), "valu_issue_util_median": round(median(util), 3),
+            "kernel_ms_median": round(median(durs), 4),
+            "method": "SQ_CYCLES / 32 engines / dispatch time; waves = SQ_WAVE_CYCLES x 4 / SQ_BUSY_CYCLES / 8 "
+                      "CUs; VALU issue = SQ_ACTIVE_INST_VALU x 4 cycles / (SQ_BUSY_CYCLES / 32 x 1,024 SIMDs)"}
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     so = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so")
@@ -102,6 +139,10 @@ def main():
                 v["GRBM_GUI_ACTIVE"] = mean(c["GRBM_GUI_ACTIVE"])
             v.update(stamp(k))
             valu[alg] = v
+    occ = occupancy(src, "kb_occ", BENCH_KERNEL["md5"])
+    if occ and "md5" in valu:
+        valu["md5"]["occupancy"] = occ
+        print("md5 occupancy", occ)
     if valu:
         json.dump({"what": "SQ_INSTS_VALU (wave-instructions) per launch of each algorithm's kernel on the bench "
                            "workload (1M x 1 KiB, fixed stride), rocprofv3 --pmc, mean over dispatches",
@@ -138,6 +179,9 @@ def main():
                "correction": "read = 2 x FETCH_SIZE, write = WRITE_SIZE (as pmc_<alg>.json)"}
         rec.update(stamp(k))
         rec["workloads"] = tiles
+        occ = occupancy(src, "kt_pktocc", k)
+        if occ:
+            rec["workloads"].setdefault("packets", {})["occupancy"] = occ
         json.dump(rec, open(os.path.join(prof, "pmc_tiles.json"), "w"), indent=1)
 
 
