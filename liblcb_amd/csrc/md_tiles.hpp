@@ -296,7 +296,7 @@ __device__ __forceinline__ uint32_t group8_or(uint32_t v) {
 // lane's count of valid chunks in the line, 4 bits each, OR-reduced in the
 // group; the group's rotations travel the same way, 2 bits each, once.
 #ifndef LCB_TILE_SKIP
-#define LCB_TILE_SKIP 0
+#define LCB_TILE_SKIP 1
 #endif
 struct TileGatherStream {
     uint8_t* slab;
@@ -333,8 +333,9 @@ struct TileGatherStream {
                                              kLdsAux);
     }
     // lastc: index of this lane's last stream chunk holding a record byte;
-    // m: its record's rotation.
-    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc, uint32_t m) {
+    // m: its record's rotation; first: its first chunk holding a record
+    // byte in line L (line 0: start >> 4 & 7; later lines 0).
+    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc, uint32_t m, uint32_t first = 0) {
         // The lane id re-defined per call: the per-lane chunk numbers below
         // are not hoisted out of the tile loop (16 VGPRs held all along).
         uint32_t ln = lane;
@@ -343,15 +344,33 @@ struct TileGatherStream {
         n = n < 0 ? 0 : (n > 8 ? 8 : n);
         const uint32_t nv = group8_or((uint32_t)n << (4u * (ln & 7u)));
         const uint32_t mpk = group_rot(m, ln);
+#if LCB_TILE_SKIP
+        const uint32_t fv = group8_or(first << (4u * (ln & 7u)));   // every lane active (DPP)
+#endif
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             const uint32_t k = (((ln & 7u) ^ (uint32_t)g) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
 #if LCB_TILE_SKIP
-            // A chunk past its record's last byte is not loaded at all (the
-            // lane is off for that DMA; its slab slot keeps stale bytes, which
-            // lie past the message end and are masked).
-            if (k < ((nv >> (4 * g)) & 15u))
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + voff[g] + L * 128u),
+            // Only the chunks that hold record bytes are fetched: a lane whose
+            // chunk lies past its record's last byte (or, in line 0, before
+            // its first) loads the nearest chunk of the line that does
+            // instead -- a 16-B piece of a line the other lanes of the same
+            // instruction fetch anyway, so no extra memory sector -- and the
+            // lanes of a record that ended in an earlier line load nothing
+            // (EXEC off: reloading any of its lines re-read HBM).  (Redirecting to the record's first chunk re-read line
+            // 0 from HBM; lanes switched off by EXEC cost the branches and the
+            // saddr form: profiles/r4_tile_skip_ab.txt.)  1M packets: HBM
+            // reads 1.237 -> 1.15 x the algorithmic bytes.
+            const uint32_t nk = (nv >> (4 * g)) & 15u, fk = (fv >> (4 * g)) & 15u;
+            const uint32_t t = k < fk ? fk : (k < nk ? k : nk - 1u);
+            const uint32_t v = voff[g] + L * 128u + 16u * t - 16u * k;
+#if LCB_TILE_SKIP == 2
+            const bool any = true;
+#else
+            const bool any = nk != 0;    // the record has bytes in line L (uniform in the lane's group)
+#endif
+            if (any)
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                                  (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
                                                  kLdsAux);
 #else
@@ -444,7 +463,10 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // (under two lines of message, the key) goes through the per-lane loop:
     // the key's window assembly next to a streamed line needs more VGPRs
     // than the occupancy leaves.  Its line count needs the whole geometry.
-    if (kMode != kTileKeyedSuffix) ls.issue_masked(0, lastc, rot());
+    if (kMode != kTileKeyedSuffix) {
+        if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
+        else ls.issue_masked(0, lastc, rot(), off >> 4);
+    }
     // The rest of the geometry: lines wholly inside every record (min),
     // blocks of the padded (virtual) message + h (max), lines whose two
     // blocks are whole message blocks (min), whole message blocks (min).
