@@ -808,6 +808,8 @@ def main():
                      "valu_floor_ms": round(vfloor, 4) if vfloor else None,
                      "valu_frac": round(vfloor / kms, 4) if vfloor else None},
     }
+    from liblcb_amd._lib import LIB_PATH
+    out["library_sha256_16"] = hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()[:16]
     clk = pmc_clock_ghz(alg)
     if vfloor and clk:
         # The same VALU floor at the clock the kernel actually runs at (the

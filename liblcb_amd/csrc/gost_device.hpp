@@ -565,6 +565,9 @@ __device__ __forceinline__ void gost_run2(G& st, const Src& src, const Tab& T) {
     uint32_t w[16];
     const uint64_t nfull = src.nfull();
     for (uint64_t j = 0; j < nfull; ++j) {
+#if LCB_LANE_PRIO
+        if ((j & 15) == 0) wave_prio_left((nfull - j) * 64u);
+#endif
         src.block(j, w);
         st.chain(w, 512, T);
     }

@@ -856,6 +856,23 @@ __device__ __forceinline__ void md_compress128(H& st, const uint32_t* a0, const 
 // the next 128 B are in flight while the current 128 B are compressed (two
 // register sets, fewer waves per SIMD); otherwise occupancy hides the load
 // latency and one set is kept.
+#ifndef LCB_LANE_PRIO
+#define LCB_LANE_PRIO 1
+#endif
+// Wave priority by the bytes its (first active) lane has left, longest
+// remaining first: s_setprio 3 / 2 / 1 / 0 at >= 48 / 32 / 16 KiB / less.
+// Among a SIMD's waves the arbiter otherwise favours the oldest, so in a
+// bucketed ragged batch (C4: 1/3 of the messages 64 KiB) the youngest long
+// waves end last and run alone at the end (md_tiles.hpp tile_prio: the
+// same rule in 128-B lines).
+__device__ __forceinline__ void wave_prio_left(uint64_t left) {
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(left >> 14 < 3 ? left >> 14 : 3));
+    if (k >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (k == 2) __builtin_amdgcn_s_setprio(2);
+    else if (k == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 template <class H, bool kPf = false>
 __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p, uint64_t nfull) {
     uint32_t w[H::kWords];
@@ -885,6 +902,9 @@ __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p
         }
     }
     for (; b < nfull; ++b, p += H::kBlock) {
+#if LCB_LANE_PRIO
+        if ((b & 15) == 0) wave_prio_left((nfull - b) * (uint64_t)H::kBlock);
+#endif
         load_block_full<H>(p, w);
         st.compress(w);
     }

@@ -1,7 +1,4 @@
-# s15: queue slots 4 vs 8 (copying and zero copy), then the round-4 PMC session.
 set -o pipefail
-O=gpurun_out/s15; mkdir -p $O
-for sl in 4 8; do for zc in 0 1; do
-  timeout -k 10 120 tools/queue_bench --alg 1 --packets 2097152 --size 1024 --threads 8 --slots $sl --zerocopy $zc > $O/q_s${sl}_zc$zc.json 2> $O/q_s${sl}_zc$zc.err; rc=$?; cut -c1-200 $O/q_s${sl}_zc$zc.json; [ $rc -ne 0 ] && exit $rc
-done; done
-TAG=r4a bash tools/pmc_session.sh
+O=gpurun_out/s21; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_packets.py -m gpu -x -q --timeout 120 --timeout-method thread -k "c4 or c3 or fixed or ragged or gost or sha512 or packets" > $O/pytest.txt 2>&1; rc=$?; tail -1 $O/pytest.txt; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u tools/ab_inproc.py --libs product,lp0 --work fixed,c4 --alg sha512,gost256 --rounds 6 > $O/ab.txt 2>&1; rc=$?; grep -v amdgpu $O/ab.txt; exit $rc
