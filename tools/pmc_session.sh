@@ -8,7 +8,7 @@
 # profiles/pmc_*.json and valu_counts.json.  Each pass has its own limit; the
 # script stops at the first failure.   TAG=r4p bash tools/pmc_session.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r4a}
+TAG=${TAG:-r4c}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
