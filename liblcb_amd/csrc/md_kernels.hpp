@@ -117,6 +117,9 @@ struct TileTrace {
 #ifndef LCB_FIXED_WAVES
 #define LCB_FIXED_WAVES 4
 #endif
+#ifndef LCB_FIXED_PRIO
+#define LCB_FIXED_PRIO 0
+#endif
 constexpr int kFixedWaves = LCB_FIXED_WAVES;   // waves (8 KiB slabs) per workgroup
 template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a) {
@@ -153,6 +156,13 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     if (nlines) ls.issue<kAux>(0);
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
+#if LCB_FIXED_PRIO
+        // longest remaining first (a wave's lines, the last ones lowest)
+        if (L == 0) __builtin_amdgcn_s_setprio(3);
+        else if (L == nlines / 4) __builtin_amdgcn_s_setprio(2);
+        else if (L == nlines / 2) __builtin_amdgcn_s_setprio(1);
+        else if (L == 3 * nlines / 4) __builtin_amdgcn_s_setprio(0);
+#endif
         ls.take(w, w + 16);                 // line L -> VGPRs, its buffer free again
         LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == nlines) tr.mark(3);)
         if (L + 1 < nlines) ls.issue<kAux>(L + 1);
