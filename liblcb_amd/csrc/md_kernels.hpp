@@ -117,8 +117,8 @@ struct TileTrace {
 #ifndef LCB_FIXED_WAVES
 #define LCB_FIXED_WAVES 4
 #endif
-#ifndef LCB_FIXED_PRIO
-#define LCB_FIXED_PRIO 0
+#ifndef LCB_FIXED_XCD
+#define LCB_FIXED_XCD 0
 #endif
 constexpr int kFixedWaves = LCB_FIXED_WAVES;   // waves (8 KiB slabs) per workgroup
 template <class H, bool kHmac, int kAux>
@@ -126,7 +126,15 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if LCB_FIXED_XCD
+    // Workgroup b runs on XCD b % 8: give each XCD one contiguous eighth of
+    // the records (its L2 / TLB see one stream) instead of every eighth group.
+    uint32_t blk = blockIdx.x;
+    if ((gridDim.x & 7u) == 0) blk = (blk & 7u) * (gridDim.x >> 3) + (blk >> 3);
+    uint64_t wave_first = ((uint64_t)blk * kFixedWaves + wv) * 64;
+#else
     uint64_t wave_first = ((uint64_t)blockIdx.x * kFixedWaves + wv) * 64;
+#endif
     // The arguments line 0's issue needs, loaded together (one scalar round
     // trip; the compiler otherwise loads the count, branches, then loads the
     // rest: two round trips before every wave's first line).
@@ -156,13 +164,6 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     if (nlines) ls.issue<kAux>(0);
     for (uint64_t L = 0; L < nlines; ++L) {
         uint32_t w[32];
-#if LCB_FIXED_PRIO
-        // longest remaining first (a wave's lines, the last ones lowest)
-        if (L == 0) __builtin_amdgcn_s_setprio(3);
-        else if (L == nlines / 4) __builtin_amdgcn_s_setprio(2);
-        else if (L == nlines / 2) __builtin_amdgcn_s_setprio(1);
-        else if (L == 3 * nlines / 4) __builtin_amdgcn_s_setprio(0);
-#endif
         ls.take(w, w + 16);                 // line L -> VGPRs, its buffer free again
         LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == nlines) tr.mark(3);)
         if (L + 1 < nlines) ls.issue<kAux>(L + 1);
