@@ -34,6 +34,9 @@ __global__ __launch_bounds__(256) void crc_batch_kernel(KArgs a) {
 // hash_device.hpp), line L+1 in flight while line L is folded in.
 // kAux: the line stream's cache policy, chosen by alignment as for the digest
 // kernels (md_fixed_lds_kernel).
+#ifndef LCB_CRC_XCD
+#define LCB_CRC_XCD 1
+#endif
 template <int V, int kAux>
 __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     using Var = CrcVar<V>;
@@ -42,7 +45,7 @@ __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     crc_stage_tables(T, Var::kFam);  // before any early return: it synchronises
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    uint64_t wave_first = ((uint64_t)(LCB_CRC_XCD ? xcd_block() : blockIdx.x) * 4 + wv) * 64;
     if (wave_first >= a.count) return;  // wave-uniform
     // A partial last wave moves back over its predecessor's records (count
     // >= 64) and stores only its own.

@@ -117,8 +117,9 @@ struct TileTrace {
 #ifndef LCB_FIXED_WAVES
 #define LCB_FIXED_WAVES 4
 #endif
+// XCD-contiguous record ranges (xcd_block).
 #ifndef LCB_FIXED_XCD
-#define LCB_FIXED_XCD 0
+#define LCB_FIXED_XCD 1
 #endif
 constexpr int kFixedWaves = LCB_FIXED_WAVES;   // waves (8 KiB slabs) per workgroup
 template <class H, bool kHmac, int kAux>
@@ -126,15 +127,7 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
     __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if LCB_FIXED_XCD
-    // Workgroup b runs on XCD b % 8: give each XCD one contiguous eighth of
-    // the records (its L2 / TLB see one stream) instead of every eighth group.
-    uint32_t blk = blockIdx.x;
-    if ((gridDim.x & 7u) == 0) blk = (blk & 7u) * (gridDim.x >> 3) + (blk >> 3);
-    uint64_t wave_first = ((uint64_t)blk * kFixedWaves + wv) * 64;
-#else
-    uint64_t wave_first = ((uint64_t)blockIdx.x * kFixedWaves + wv) * 64;
-#endif
+    uint64_t wave_first = ((uint64_t)(LCB_FIXED_XCD ? xcd_block() : blockIdx.x) * kFixedWaves + wv) * 64;
     // The arguments line 0's issue needs, loaded together (one scalar round
     // trip; the compiler otherwise loads the count, branches, then loads the
     // rest: two round trips before every wave's first line).

@@ -25,14 +25,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import liblcb_amd  # noqa: E402
-from liblcb_amd._lib import ALG_IDS, DIGEST_SIZE, F_DEVICE, SIGNATURES  # noqa: E402
+from liblcb_amd._lib import ALG_IDS, CRC_SIGNATURES, DIGEST_SIZE, F_DEVICE, SIGNATURES  # noqa: E402
+from liblcb_amd.crc32 import CRC_NAMES  # noqa: E402
+
+CRC_IDS = {n: v for v, n in CRC_NAMES.items()}
 
 
 def load(name):
     path = os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so") if name == "product" else \
         os.path.join(ROOT, "build_exp", name, "liblcb_hash_gpu.so")
     L = ctypes.CDLL(path)
-    for fn, res, args in SIGNATURES:
+    for fn, res, args in SIGNATURES + CRC_SIGNATURES:
         if hasattr(L, fn):
             f = getattr(L, fn)
             f.restype = res
@@ -78,15 +81,22 @@ def main():
         do = torch.as_tensor(offs.astype(np.int64), device="cuda") if offs is not None else None
         dl = torch.as_tensor(lens.astype(np.int32), device="cuda") if lens is not None else None
         for alg_name in a.alg.split(","):
-            alg = ALG_IDS[alg_name]
-            dig = torch.empty((count, DIGEST_SIZE[alg]), dtype=torch.uint8, device="cuda")
+            crc = CRC_IDS.get(alg_name)      # a CRC-32 variant (lcb_crc32_batch) or a hash
+            alg = None if crc else ALG_IDS[alg_name]
+            dig = torch.empty((count, 4 if crc else DIGEST_SIZE[alg]), dtype=torch.uint8, device="cuda")
             launches = max(4, a.launches if wname in ("fixed", "r1k") else a.launches // (10 if wname == "c4" else 2))
 
             def run(L, k):
                 for _ in range(k):
-                    rc = L.lcb_hash_batch(alg, None, 0, data.data_ptr(), do.data_ptr() if do is not None else None,
-                                          dl.data_ptr() if dl is not None else None, count, stride, stride,
-                                          dig.data_ptr(), F_DEVICE, s.cuda_stream)
+                    if crc:
+                        rc = L.lcb_crc32_batch(crc, None, data.data_ptr(),
+                                               do.data_ptr() if do is not None else None,
+                                               dl.data_ptr() if dl is not None else None, count, stride, stride,
+                                               dig.data_ptr(), F_DEVICE, s.cuda_stream)
+                    else:
+                        rc = L.lcb_hash_batch(alg, None, 0, data.data_ptr(), do.data_ptr() if do is not None else None,
+                                              dl.data_ptr() if dl is not None else None, count, stride, stride,
+                                              dig.data_ptr(), F_DEVICE, s.cuda_stream)
                     if rc:
                         raise SystemExit("lcb_hash_batch rc=%d" % rc)
             res = {n: [] for n in libs}
