@@ -8,6 +8,8 @@
 // No inter-workgroup communication; every message is independent.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
+
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
 
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(256, kPf ? 1 : H::kOcc) void md_batch_kernel(KArgs 
 // + two per-lane offsets, no VALU per DMA) while the two 64-B blocks of line
 // L are compressed.  Bytes after the last whole line go through the generic
 // loader.  One line in flight per wave (8 KiB of LDS), 4 waves per workgroup,
-// 5 workgroups per CU (the whole 160 KiB); deeper per-wave buffering,
+// 4 workgroups per CU (128 KiB; a fifth is never placed); deeper per-wave buffering,
 // half-line stages and taking the next line mid-way through the current one
 // (two line registers sets: 4 waves/SIMD) measured slower
 // (profiles/r1_lds_depth_ab.txt, r1_lds_half_ab.txt, r2_fixed_stream_ab.txt).
@@ -121,7 +123,139 @@ struct TileTrace {
 #ifndef LCB_FIXED_XCD
 #define LCB_FIXED_XCD 1
 #endif
+// Resident-grid form (MD5; LCB_FIXED_PERSIST = workgroups per CU, 0 = off):
+// the grid is exactly the workgroups that fit at once (4 x 32 KiB per CU, the
+// fifth is never placed: DESIGN.md 9.5), XCD x owns the x-th eighth of the
+// 64-record chunks and its waves sweep it together (chunk = base + slot +
+// j * slots, so every SIMD hashes the same number of chunks), the next
+// chunk's line 0 is issued while the current chunk's last line is
+// compressed, and each wave's priority is the chunks it has left
+// (LCB_FIXED_PPRIO: the arbiter otherwise favours the oldest wave, which
+// ends first and leaves its SIMD one wave short at the end).  Same-process
+// A/B against the one-generation-per-workgroup kernel (profiles/
+// r4_fixed_persist_ab.txt): MD5 -1.9 %; contiguous runs per wave -0.4 %,
+// without the priority +1.2 / +1.7 %; SHA-1 / SHA-256 +-0.2 % (not used).
+#ifndef LCB_FIXED_PERSIST
+#define LCB_FIXED_PERSIST 4
+#endif
+#ifndef LCB_FIXED_PPRIO
+#define LCB_FIXED_PPRIO 1
+#endif
+#ifndef LCB_FIXED_PINTER
+#define LCB_FIXED_PINTER 1
+#endif
 constexpr int kFixedWaves = LCB_FIXED_WAVES;   // waves (8 KiB slabs) per workgroup
+constexpr int kFixedPersist = LCB_FIXED_PERSIST;
+
+template <class H, bool kHmac>
+__device__ __forceinline__ void md_fixed_finish(H& st, const KArgs& a, const uint8_t* data, uint64_t stride,
+                                                uint32_t fixed_len, uint64_t nlines, uint64_t prefix,
+                                                uint64_t wave_first, uint32_t skip, uint32_t lane) {
+    if (lane < skip) return;
+    const uint64_t i = wave_first + lane;
+    const uint8_t* msg = data + i * stride + nlines * 128;
+    const uint64_t tail = (uint64_t)fixed_len - nlines * 128;
+    if (tail == 0)  // wave-uniform: schedule of the pad block on the SALU
+        md_pad_only(st, prefix + nlines * 128);
+    else
+        md_message(st, msg, tail, prefix + nlines * 128);
+    uint32_t dw[H::kDigest / 4];
+    st.digest_words(dw);
+    if (kHmac) {
+        H o;
+        load_words(o.s, a.mid + kMidWords);
+        md_outer(o, dw);
+        o.digest_words(dw);
+    }
+    store_digest<H::kDigest>(a.digests + i * H::kDigest, dw);
+}
+
+template <class H, bool kHmac, int kAux>
+__global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint8_t* data = a.data;
+    uint64_t count = a.count, stride = a.stride;
+    uint32_t fixed_len = a.fixed_len;
+    asm volatile("" : "+s"(data), "+s"(count), "+s"(stride), "+s"(fixed_len));
+    // Balanced contiguous chunk range of this wave slot.
+    const uint64_t nch = (count + 63) / 64;
+#if LCB_FIXED_PINTER
+    // Interleaved: XCD x owns the x-th eighth of the chunks; its waves sweep
+    // it together (chunk base + slot + j * slots).
+    const uint64_t xcd = blockIdx.x & 7u, nbx = gridDim.x >> 3;
+    const uint64_t xb = xcd * nch / 8, xe = (xcd + 1) * nch / 8;
+    const uint64_t lslots = nbx * kFixedWaves;
+    const uint64_t ls0 = (uint64_t)(blockIdx.x >> 3) * kFixedWaves + wv;
+    uint64_t c = xb + ls0;
+    const uint64_t cstep = lslots;
+    const uint64_t c_end = c < xe ? c + (xe - 1 - c) / cstep * cstep + cstep : c;
+#else
+    const uint64_t slots = (uint64_t)gridDim.x * kFixedWaves;
+    const uint64_t s = (uint64_t)xcd_block() * kFixedWaves + wv;
+    uint64_t c = s * nch / slots;
+    const uint64_t c_end = (s + 1) * nch / slots;
+    constexpr uint64_t cstep = 1;
+#endif
+    if (c >= c_end) return;  // wave-uniform
+    const uint64_t last = count - 1;
+    const uint64_t nlines = fixed_len / 128;
+    // A partial last chunk moves back over its predecessor's records (count
+    // >= 64) and stores only its own.
+    auto first_of = [&](uint64_t ch, uint32_t& sk) {
+        uint64_t f = ch * 64;
+        sk = f + 63 > last ? (uint32_t)(f + 63 - last) : 0u;
+        return f - sk;
+    };
+    uint32_t skip;
+    uint64_t wave_first = first_of(c, skip);
+    LdsStridedStream ls;
+    ls.init(data, stride, wave_first, lane, &slab[wv][0]);
+    ls.issue<kAux>(0);
+    for (;;) {
+        H st;
+        uint64_t prefix = 0;
+        if (kHmac) {
+            load_words(st.s, a.mid);
+            prefix = H::kBlock;
+        } else {
+            st.init();
+        }
+        const bool more = c + cstep < c_end;
+        uint32_t nskip = 0;
+        const uint64_t next_first = more ? first_of(c + cstep, nskip) : 0;
+        for (uint64_t L = 0; L < nlines; ++L) {
+            uint32_t w[32];
+            if (LCB_FIXED_PPRIO) {
+                const uint64_t left = (c_end - c) / cstep * nlines - L;
+                if (left >= 3 * nlines) __builtin_amdgcn_s_setprio(3);
+                else if (left >= 2 * nlines) __builtin_amdgcn_s_setprio(2);
+                else if (left >= nlines) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+            ls.take(w, w + 16);
+            if (L + 1 < nlines) {
+                ls.issue<kAux>(L + 1);
+            } else if (more) {                  // the next chunk's line 0
+                ls.wbase = data + next_first * stride;
+                ls.issue<kAux>(0);
+            }
+            if constexpr (H::kBlock == 128) {
+                st.compress(w);
+            } else {
+                st.compress(w);
+                st.compress(w + 16);
+            }
+        }
+        md_fixed_finish<H, kHmac>(st, a, data, stride, fixed_len, nlines, prefix, wave_first, skip, lane);
+        if (!more) break;
+        c += cstep;
+        wave_first = next_first;
+        skip = nskip;
+    }
+}
+
 template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
@@ -316,6 +450,20 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
         if (fixed_stride_lines(a)) {
             constexpr unsigned T = 64 * kFixedWaves;
             const dim3 grid((unsigned)((a.count + T - 1) / T));
+            if constexpr (kFixedPersist > 0 && std::is_same<H, Md5>::value) {
+                const uint64_t cap = (uint64_t)kFixedPersist * device_cu_count();
+                if (grid.x > cap && cap % 8 == 0) {
+                    const dim3 pg((unsigned)cap);
+                    if (a.stride % 128 == 0 && reinterpret_cast<uintptr_t>(a.data) % 128 == 0) {
+                        if (hmac) hipLaunchKernelGGL((md_fixed_persist_kernel<H, true, kLdsAux>), pg, dim3(T), 0, s, a);
+                        else hipLaunchKernelGGL((md_fixed_persist_kernel<H, false, kLdsAux>), pg, dim3(T), 0, s, a);
+                    } else {
+                        if (hmac) hipLaunchKernelGGL((md_fixed_persist_kernel<H, true, kGatherAux>), pg, dim3(T), 0, s, a);
+                        else hipLaunchKernelGGL((md_fixed_persist_kernel<H, false, kGatherAux>), pg, dim3(T), 0, s, a);
+                    }
+                    return;
+                }
+            }
             if (a.stride % 128 == 0 && reinterpret_cast<uintptr_t>(a.data) % 128 == 0) {
                 if (hmac) hipLaunchKernelGGL((md_fixed_lds_kernel<H, true, kLdsAux>), grid, dim3(T), 0, s, a);
                 else hipLaunchKernelGGL((md_fixed_lds_kernel<H, false, kLdsAux>), grid, dim3(T), 0, s, a);

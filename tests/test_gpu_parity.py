@@ -185,6 +185,23 @@ def test_fixed_stride_partial_last_wave(gpu, oracle, count):
         assert np.array_equal(got, np.asarray(exp).view(np.uint32)), ("crc", count, stride, flen)
 
 
+@pytest.mark.parametrize("count", [4 * 256 * 256 + 1, 4 * 256 * 256 + 64 * 8 * 3 + 37, 300000])
+def test_fixed_stride_resident_grid(gpu, oracle, count):
+    """MD5 batches larger than one resident grid (4 workgroups x 256 CUs x
+    256 records) take md_fixed_persist_kernel: every wave hashes several
+    64-record chunks of its XCD's eighth, the partial last chunk moved back.
+    Uneven chunk counts per XCD and per wave, both line-stream policies
+    (128-B aligned stride: nt; 16-B: default), whole-line and ragged tails,
+    plain and HMAC, all digests vs the oracle."""
+    for stride, flen in ((256, 256), (208, 200)):
+        data = gen_stream(count + flen, count * stride)
+        dd = dev(data)
+        for key in (None, b"radius-secret"):
+            exp = oracle.batch(1, data, count=count, stride=stride, fixed_len=flen, key=key)
+            got = gpu.hash_batch(1, dd, count=count, stride=stride, fixed_len=flen, key=key).cpu().numpy()
+            assert np.array_equal(got, exp), (count, stride, flen, key)
+
+
 def test_bit_length_high_word(gpu, oracle):
     """A message of 512 MiB + 67 B: its bit length no longer fits 32 bits, so
     the high word of MD5's LE length field (md5.h:282) and of SHA-512's

@@ -27,7 +27,7 @@ def rows():
 
 def test_every_kernel_listed(rows):
     names = [r["name"] for r in rows]
-    for k in ("md_fixed_lds_kernel", "md_batch_kernel", "md_tiles_kernel", "md_keyed_kernel",
+    for k in ("md_fixed_lds_kernel", "md_fixed_persist_kernel", "md_batch_kernel", "md_tiles_kernel", "md_keyed_kernel",
               "gost_plain2_kernel", "gost_hmac_kernel", "gost_keyed_kernel", "bucket_place_kernel", "crc_fixed_lds_kernel",
               "chacha_lane_kernel"):
         assert any(k in n for n in names), (k, sorted(names)[:20])

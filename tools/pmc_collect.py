@@ -30,7 +30,7 @@ CXXFILT = "c++filt"
 # The kernel each algorithm launches on the bench workload (1M x 1 KiB,
 # 128-B aligned stride: the nt line stream, aux 2).
 BENCH_KERNEL = {
-    "md5": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Md5, false, 2>",
+    "md5": "lcbgpu::md_fixed_persist_kernel<lcbgpu::Md5, false, 2>",
     "sha1": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha1, false, 2>",
     "sha224": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha256<true>, false, 2>",
     "sha256": "lcbgpu::md_fixed_lds_kernel<lcbgpu::Sha256<false>, false, 2>",
