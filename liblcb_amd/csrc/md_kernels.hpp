@@ -322,6 +322,82 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
               tr.put(g_fixed_trace, trw, lane == skip ? 0u : 1u);)
 }
 
+// ------------------------- ragged 128-B-block batches (SHA-384/512), streamed
+// A bucketed ragged batch (order by length class) of a 128-B-block hash: wave
+// = 64 consecutive order entries, lane = message.  When every record of the
+// wave starts 16-B aligned, the first nmin lines (nmin = the wave's smallest
+// whole-line count; every record has them) stream through the wave's LDS
+// slab with coalesced LDS-DMA (GatherLineStream: 8 records x one 128-B line
+// per instruction, line L + 1 issued while line L is compressed: one line =
+// one SHA-512 block); the rest of each message (further whole blocks, tail,
+// padding) takes the per-lane loop.  The per-lane loop alone (md_batch_kernel
+// over the order) streams each lane's message from its own address: with
+// C4's 64 KiB records every lane of a wave reads a different page per block.
+// Default cache policy: a record at a 64-B offset straddles cache lines, the
+// second half stays in L2 for the record's next line.
+#ifndef LCB_LINES128
+#define LCB_LINES128 1
+#endif
+template <class H, bool kHmac>
+__global__ __launch_bounds__(256, 4) void md_lines_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    if (first >= a.count) return;  // wave-uniform
+    const uint64_t i = first + lane;
+    const bool valid = i < a.count;
+    // A lane past the batch end takes the wave's first record (no pad entries:
+    // the order of a 128-B-block batch is unpadded), so every DMA address is a
+    // record's own line.
+    const uint64_t idx = gptr(a.order)[valid ? i : first];
+    const uint8_t* msg = gptr(a.data) + (a.offsets ? gptr(a.offsets)[idx] : idx * a.stride);
+    const uint64_t len = gptr(a.lengths)[idx];
+    // Wave minimum of the whole-line counts (0 unless every record is 16-B
+    // aligned), every lane active.
+    uint32_t m = (reinterpret_cast<uintptr_t>(msg) & 15u) ? 0u : (uint32_t)(len >> 7);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t t = (uint32_t)__shfl_xor((int)m, o, 64);
+        m = t < m ? t : m;
+    }
+    const uint32_t nmin = (uint32_t)__builtin_amdgcn_readfirstlane(m);
+    H st;
+    uint64_t prefix = 0;
+    if (kHmac) {
+        load_words(st.s, a.mid);
+        prefix = H::kBlock;
+    } else {
+        st.init();
+    }
+    if (nmin) {
+        GatherLineStream ls;
+        ls.init_gather(msg, nmin - 1, lane, &slab[wv][0]);
+        ls.issue_next_uniform<kGatherAux>();
+        for (uint32_t L = 0; L < nmin; ++L) {
+#if LCB_LANE_PRIO
+            if ((L & 15) == 0) wave_prio_left((uint64_t)(nmin - L) * 128);
+#endif
+            uint32_t w[32];
+            ls.take(w, w + 16);
+            if (L + 1 < nmin) ls.issue_next_uniform<kGatherAux>();
+            st.compress(w);
+        }
+    }
+    if (!valid) return;
+    const uint64_t done = (uint64_t)nmin * 128;
+    md_message(st, msg + done, len - done, prefix + done);
+    uint32_t dw[H::kDigest / 4];
+    st.digest_words(dw);
+    if (kHmac) {
+        H o;
+        load_words(o.s, a.mid + kMidWords);
+        md_outer(o, dw);
+        o.digest_words(dw);
+    }
+    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
+}
+
 }  // namespace lcbgpu
 #include "md_tiles.hpp"
 namespace lcbgpu {
@@ -476,6 +552,15 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
     }
     if (a.order && a.tile_next) {  // bucketed ragged batch: the tile kernel
         if (hmac ? launch_tiles<H, kTileHmac>(a, s) : launch_tiles<H, kTilePlain>(a, s)) return;
+    }
+    if constexpr (H::kBlock == 128 && LCB_LINES128) {
+        // bucketed (unpadded order) 128-B-block batch: the streamed line loop
+        if (a.order && a.lengths && !a.tile_next && a.count >= kPfMaxCount) {
+            const dim3 grid((unsigned)((a.count + 255) / 256));
+            if (hmac) hipLaunchKernelGGL((md_lines_kernel<H, true>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((md_lines_kernel<H, false>), grid, dim3(256), 0, s, a);
+            return;
+        }
     }
     if (a.count < kPfMaxCount) {
         if (hmac) hipLaunchKernelGGL((md_batch_kernel<H, true, true>), grid_for(a.count), dim3(256), 0, s, a);

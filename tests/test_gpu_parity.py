@@ -185,6 +185,36 @@ def test_fixed_stride_partial_last_wave(gpu, oracle, count):
         assert np.array_equal(got, np.asarray(exp).view(np.uint32)), ("crc", count, stride, flen)
 
 
+@pytest.mark.parametrize("layout", ["aligned64", "aligned16", "packed"])
+def test_sha512_ragged_line_stream(gpu, oracle, layout):
+    """Bucketed ragged SHA-384/512 batches (count >= 16,384) take
+    md_lines_kernel: waves whose records all start 16-B aligned stream their
+    common whole lines through LDS, then finish per lane; other waves (packed:
+    most) take the per-lane loop from line 0.  Lengths 0..3000, runs of equal
+    lengths (C4-like), some 64 KiB records, a partial last wave; plain and
+    HMAC vs the oracle."""
+    rng = np.random.default_rng(7 + len(layout))
+    n = 20000 + 37
+    lens = rng.integers(0, 3001, n).astype(np.uint32)
+    lens[: n // 4] = 1024
+    lens[rng.integers(0, n, 60)] = 65536
+    lens[rng.integers(0, n, 60)] = 128 * rng.integers(1, 9, 60)
+    align = {"aligned64": 64, "aligned16": 16, "packed": 1}[layout]
+    offs = np.zeros(n, np.uint64)
+    pos = 0
+    for k in range(n):
+        pos = (pos + align - 1) // align * align
+        offs[k] = pos
+        pos += int(lens[k]) + (int(rng.integers(0, 3)) if layout == "packed" else 0)
+    data = gen_stream(123 + align, pos + 16)
+    dd, dl, do = dev(data), dev(lens, np.int32), dev(offs, np.int64)
+    for alg in (5, 6):
+        for key in (None, b"radius-secret"):
+            exp = oracle.batch(alg, data, offs, lens, key=key)
+            got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=key).cpu().numpy()
+            assert np.array_equal(got, exp), (layout, alg, key)
+
+
 @pytest.mark.parametrize("count", [4 * 256 * 256 + 1, 4 * 256 * 256 + 64 * 8 * 3 + 37, 300000])
 def test_fixed_stride_resident_grid(gpu, oracle, count):
     """MD5 batches larger than one resident grid (4 workgroups x 256 CUs x

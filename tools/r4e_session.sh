@@ -1,5 +1,6 @@
 #!/bin/bash
-# Closing GPU session of the resident-grid MD5 build: smoke, GPU tests, the
+# Closing GPU session of the resident-grid MD5 build: the SHA-384/512 line-
+# stream A/B (when build_exp/nolines exists), smoke, GPU tests, the
 # PMC passes (tools/pmc_session.sh) collected into the stamped counter files
 # on the box, then the bench (which reads them) and its kernel trace.
 # Stops at the first failure.   TAG=r4e bash tools/r4e_session.sh
@@ -8,6 +9,10 @@ TAG=${TAG:-r4e}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+if [ -d build_exp/nolines ]; then
+  timeout -k 10 300 python -u tools/ab_inproc.py --libs product,nolines --work c4,r1k,pkt --alg sha512,sha384 --rounds 10 > $O/ab_lines.txt 2>&1
+  rc=$?; echo "ab rc=$rc"; grep -v amdgpu $O/ab_lines.txt | cut -c1-330; [ $rc -ne 0 ] && exit $rc
+fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.txt 2>&1
