@@ -473,8 +473,9 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
     mix64(seed + i) % 3, packed, device resident.  The library
     buckets the ragged batch by length on the device (counted in the time).
     One pass per algorithm of `algs` over the same bytes (the first is the
-    headline; MD5, SHA-1 and SHA-224/256 run the tile kernel, SHA-384/512 and
-    GOST the per-lane kernel over the bucketed order), each checked against
+    headline; MD5, SHA-1 and SHA-224/256 run the tile kernel, SHA-384/512 the
+    LDS line stream and GOST the per-lane kernel over the bucketed order),
+    each checked against
     the reference's digest-of-digests."""
     from tests.golden_util import mixed_lengths
     lens = np.array(mixed_lengths(SEED, count), dtype=np.uint32)
@@ -881,13 +882,24 @@ def main():
         c4 = bench_c4([alg] + [ALG_IDS[n] for n in ("sha1", "sha256", "sha512", "gost256") if ALG_IDS[n] != alg],
                       a.warmup, max(3, a.steps // 4))
         out["ragged_c4"] = c4.pop(ALG_NAMES[alg])
-        # The other algorithms on C4 (SHA-1/256: the tile kernel; SHA-512,
-        # GOST: per-lane kernels over the bucketed order), with their
-        # fixed-stride rate for comparison: VALU-bound, so ragged ~ fixed
-        # means the ragged machinery is hidden.
+        # The other algorithms on C4 (SHA-1/256: the tile kernel; SHA-512:
+        # the LDS line stream over the bucketed order; GOST: the per-lane
+        # kernel), with their fixed-stride rate for comparison: VALU-bound, so
+        # ragged ~ fixed means the ragged machinery is hidden.  The per-block
+        # ratio also counts the compressions each byte costs (C4's padding
+        # blocks are ~0.3 % of its bytes, 1 KiB records' 6 % / 12.5 %).
+        from tests.golden_util import mixed_lengths_np
+        c4_lens = mixed_lengths_np(SEED, MSGS_PER_GPU).astype(np.uint64)
         for name, r in c4.items():
             if name in per:
                 r["fixed_stride_GiB_s"] = per[name]["GiB_s"]
+                blk = {"sha384": (128, 16), "sha512": (128, 16)}.get(name, (64, 8))
+                if not name.startswith("gost"):
+                    def blocks_per_byte(lens):
+                        return float(((lens + 1 + blk[1] + blk[0] - 1) // blk[0]).sum() * blk[0]) / float(lens.sum())
+                    r["fixed_stride_ratio_per_block"] = round(
+                        r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
+                        blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
         out["ragged_c4_per_alg"] = c4
         out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4))
         out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
