@@ -190,17 +190,19 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArg
     const uint64_t ls0 = (uint64_t)(blockIdx.x >> 3) * kFixedWaves + wv;
     uint64_t c = xb + ls0;
     const uint64_t cstep = lslots;
-    const uint64_t c_end = c < xe ? c + (xe - 1 - c) / cstep * cstep + cstep : c;
+    if (c >= xe) return;  // wave-uniform
+    uint32_t nleft = (uint32_t)((xe - 1 - c) / cstep + 1);   // chunks left, this one included
 #else
     const uint64_t slots = (uint64_t)gridDim.x * kFixedWaves;
     const uint64_t s = (uint64_t)xcd_block() * kFixedWaves + wv;
     uint64_t c = s * nch / slots;
     const uint64_t c_end = (s + 1) * nch / slots;
     constexpr uint64_t cstep = 1;
-#endif
     if (c >= c_end) return;  // wave-uniform
+    uint32_t nleft = (uint32_t)(c_end - c);
+#endif
     const uint64_t last = count - 1;
-    const uint64_t nlines = fixed_len / 128;
+    const uint32_t nlines = fixed_len / 128;
     // A partial last chunk moves back over its predecessor's records (count
     // >= 64) and stores only its own.
     auto first_of = [&](uint64_t ch, uint32_t& sk) {
@@ -222,18 +224,17 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArg
         } else {
             st.init();
         }
-        const bool more = c + cstep < c_end;
+        const bool more = nleft > 1;
         uint32_t nskip = 0;
         const uint64_t next_first = more ? first_of(c + cstep, nskip) : 0;
-        for (uint64_t L = 0; L < nlines; ++L) {
+        if (LCB_FIXED_PPRIO) {  // once per chunk: the chunks left after this one
+            if (nleft > 3) __builtin_amdgcn_s_setprio(3);
+            else if (nleft == 3) __builtin_amdgcn_s_setprio(2);
+            else if (nleft == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        for (uint32_t L = 0; L < nlines; ++L) {
             uint32_t w[32];
-            if (LCB_FIXED_PPRIO) {
-                const uint64_t left = (c_end - c) / cstep * nlines - L;
-                if (left >= 3 * nlines) __builtin_amdgcn_s_setprio(3);
-                else if (left >= 2 * nlines) __builtin_amdgcn_s_setprio(2);
-                else if (left >= nlines) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
             ls.take(w, w + 16);
             if (L + 1 < nlines) {
                 ls.issue<kAux>(L + 1);
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArg
         }
         md_fixed_finish<H, kHmac>(st, a, data, stride, fixed_len, nlines, prefix, wave_first, skip, lane);
         if (!more) break;
+        --nleft;
         c += cstep;
         wave_first = next_first;
         skip = nskip;

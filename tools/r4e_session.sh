@@ -9,7 +9,11 @@ TAG=${TAG:-r4e}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-if [ -d build_exp/nolines ]; then
+# AB_LIBS=product,<build_exp name> AB_WORK=... AB_ALG=...: a same-process A/B first.
+if [ -n "$AB_LIBS" ]; then
+  timeout -k 10 300 python -u tools/ab_inproc.py --libs $AB_LIBS --work ${AB_WORK:-fixed} --alg ${AB_ALG:-md5} --rounds ${AB_ROUNDS:-12} > $O/ab.txt 2>&1
+  rc=$?; echo "ab rc=$rc"; grep -v amdgpu $O/ab.txt | cut -c1-330; [ $rc -ne 0 ] && exit $rc
+elif [ -d build_exp/nolines ]; then
   timeout -k 10 300 python -u tools/ab_inproc.py --libs product,nolines --work c4,r1k,pkt --alg sha512,sha384 --rounds 10 > $O/ab_lines.txt 2>&1
   rc=$?; echo "ab rc=$rc"; grep -v amdgpu $O/ab_lines.txt | cut -c1-330; [ $rc -ne 0 ] && exit $rc
 fi
