@@ -714,7 +714,10 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // 4.70 default; profiles/r2_c4_tiles_ab.txt).  Tiles whose records share
 // a 0 or 64-B phase stream whole cache lines with nt instead (md_tile_stream).
 constexpr int kGatherAux = 0;
-constexpr int kLdsAux = 2;  // cache policy of the LDS-DMA stream: nt (every byte is read once)
+#ifndef LCB_LDS_AUX
+#define LCB_LDS_AUX 2
+#endif
+constexpr int kLdsAux = LCB_LDS_AUX;  // cache policy of the LDS-DMA stream: nt (every byte is read once)
 // The slab side shared by the line streams: take() copies this lane's 128 B
 // of the landed line into VGPRs.
 struct LdsLineSlab {
