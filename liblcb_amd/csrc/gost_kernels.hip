@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kGostThreads) void gost_keyed_kernel(KArgs a) {
     }
     st.digest_words(dw, T);
     settle_words<G::kDigest / 4>(dw);
-    store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
+    if (!batch_aborted(a)) store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
     }
 }
 

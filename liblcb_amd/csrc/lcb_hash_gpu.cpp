@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <mutex>
 #include <thread>
@@ -89,39 +90,262 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
 
 hipError_t scratch_free(void* p, hipStream_t s) { return hipFreeAsync(p, s); }
 
-// HMAC: build the key block / long-key buffer and enqueue the mid-state prep
-// kernel.  *mid receives a scratch allocation the caller frees with
-// scratch_free after the batch kernel.
-int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
-               uint8_t** dkey_out) {
+// ------------------------------------------------------ per-stream scratch
+// Every stream-ordered allocation, free or event record costs ~6.5 us of the
+// stream's timeline (the marker packet it enqueues; rocprofv3 traces of the
+// 1M-packet pass, profiles/r5_pkt_gaps.txt: 6.6 us of idle before the first
+// bucketing kernel with one allocation, 12.2 us with two, 6.2 us after an
+// hipEventRecord), i.e. 1-2 % of a packet pass.  Each (device, stream)
+// keeps ONE buffer instead, reused by the batches enqueued on that stream:
+// the stream's order puts every use after the previous one, so nothing is
+// recorded per call.  A call holds the buffer exclusively while it enqueues
+// (another thread enqueueing on the same stream at that moment takes the
+// pool path).  Streams are told apart by handle: a destroyed stream's object
+// is released only once its work has completed, so a later stream that
+// reuses the handle finds the buffer idle (hipStreamPerThread names a
+// different stream in every thread: it takes the pool path).  Buffers are
+// never evicted: past kStreamScratchMax streams, new ones take the pool
+// path.  A buffer that grows is retired with an event (the one record) and
+// freed once that event has completed.
+// Header (kStreamScratchHeader bytes): word 0 = the key-index check's flag
+// (the call's epoch when an index is bad), word 1 = the check kernel's
+// block counter (monotonic; the host tracks its expected value).
+struct StreamScratch {
+    int dev = -1;
+    hipStream_t sid = nullptr;
+    uint8_t* p = nullptr;          // device: [header | payload]
+    size_t bytes = 0;              // payload bytes
+    uint32_t* hflag = nullptr;     // pinned coherent host word: check result (epoch | bad bit)
+    uint32_t epoch = 0;            // last check epoch used on this buffer (< 2^31)
+    uint32_t ctr = 0;              // expected value of header word 1
+    bool busy = false;
+};
+constexpr size_t kStreamScratchHeader = 256;
+constexpr size_t kStreamScratchMax = 16;
+
+namespace {
+std::mutex g_ss_mu;
+std::vector<StreamScratch*> g_ss;
+std::vector<std::pair<uint8_t*, hipEvent_t>> g_ss_retired;
+
+void ss_reap_locked() {
+    for (size_t k = 0; k < g_ss_retired.size();) {
+        if (hipEventQuery(g_ss_retired[k].second) == hipSuccess) {
+            (void)hipFree(g_ss_retired[k].first);
+            (void)hipEventDestroy(g_ss_retired[k].second);
+            g_ss_retired.erase(g_ss_retired.begin() + k);
+        } else {
+            (void)hipGetLastError();
+            ++k;
+        }
+    }
+}
+}  // namespace
+
+StreamScratch* stream_scratch_acquire(hipStream_t s, size_t bytes) {
+    int dev = 0;
+    if (s == hipStreamPerThread || hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ss_mu);
+    if (!g_ss_retired.empty()) ss_reap_locked();
+    StreamScratch* e = nullptr;
+    for (StreamScratch* x : g_ss)
+        if (x->dev == dev && x->sid == s) { e = x; break; }
+    if (e && e->busy) return nullptr;   // another thread is enqueueing on this stream
+    if (!e) {
+        if (g_ss.size() >= kStreamScratchMax) return nullptr;
+        e = new StreamScratch();
+        if (hipHostMalloc(reinterpret_cast<void**>(&e->hflag), 64, hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            delete e;
+            return nullptr;
+        }
+        *e->hflag = 0;
+        e->dev = dev;
+        e->sid = s;
+        g_ss.push_back(e);
+    }
+    if (e->bytes < bytes || !e->p) {
+        // Grow (to 1.25x, so a slowly growing batch does not reallocate every
+        // call); the old buffer is freed once the work enqueued so far is done.
+        if (e->p) {
+            hipEvent_t ev = nullptr;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(ev, s) != hipSuccess) {
+                (void)hipGetLastError();
+                if (ev) (void)hipEventDestroy(ev);
+                return nullptr;
+            }
+            g_ss_retired.emplace_back(e->p, ev);
+            e->p = nullptr;
+            e->bytes = 0;
+        }
+        const size_t nb = std::max<size_t>(bytes + bytes / 4, 1u << 20);
+        if (hipMalloc(reinterpret_cast<void**>(&e->p), nb + kStreamScratchHeader) != hipSuccess) {
+            (void)hipGetLastError();
+            e->p = nullptr;
+            return nullptr;
+        }
+        // Header zeroed in stream order: flag 0 (epochs start at 1), counter 0.
+        if (hipMemsetAsync(e->p, 0, kStreamScratchHeader, s) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(e->p);
+            e->p = nullptr;
+            return nullptr;
+        }
+        e->bytes = nb;
+        e->ctr = 0;
+    }
+    e->busy = true;
+    return e;
+}
+
+uint8_t* stream_scratch_payload(StreamScratch* e) { return e->p + kStreamScratchHeader; }
+
+void stream_scratch_release(StreamScratch* e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(g_ss_mu);
+    e->busy = false;
+}
+
+// ------------------------------------------------------------- key cache
+// Key tables of keyed batches (lcb_hash_batch_keyed) and single HMAC keys
+// (lcb_hash_batch with a key), uploaded and prepared (mid-states) once per
+// device and reused while the same keys come back: a RADIUS server signs
+// every batch with the same table of peer secrets (radius_client.c:242,886,
+// 1025), and the upload (three pageable copies) plus the prep kernel cost
+// ~30 us of stream time per call (r5 trace).  Entries are looked up by their
+// exact bytes; at most kKeyCacheMax live per process (further tables take
+// the per-call path).  An entry is immutable once prepared; a stream other
+// than the one that prepared it waits on its `ready` event.
+struct KeyCacheEntry {
+    int dev = -1;
+    int alg = 0;
+    int kind = 0;                    // LCB_HASH_KEY_* of a table, or 0: one HMAC key
+    std::vector<uint8_t> sig;        // key bytes + lengths (the lookup key)
+    uint8_t* dbuf = nullptr;         // [key bytes | key offsets | key lengths | mid-states]
+    KeyTable kt;
+    hipEvent_t ready = nullptr;
+    hipStream_t sid = nullptr;       // stream that prepared it
+};
+constexpr size_t kKeyCacheMax = 16;
+namespace {
+std::mutex g_kc_mu;
+std::vector<KeyCacheEntry*> g_kc;
+}  // namespace
+
+// The device key table of (alg, kind, keys): cached or built on `s`.  *temp
+// = a per-call buffer the caller releases with scratch_free after the batch
+// (the cache is full), else null.
+static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const std::vector<uint32_t>& koff,
+                     const std::vector<uint32_t>& klen, const KeyBlock* kb, hipStream_t s, KeyTable* out,
+                     uint8_t** temp) {
+    *temp = nullptr;
+    int dev = 0;
+    LCB_TRY(hipGetDevice(&dev));
+    const hipStream_t sid = s;
+    std::vector<uint8_t> sig(blob.begin(), blob.end());
+    sig.insert(sig.end(), reinterpret_cast<const uint8_t*>(klen.data()),
+               reinterpret_cast<const uint8_t*>(klen.data() + klen.size()));
+    std::lock_guard<std::mutex> lk(g_kc_mu);
+    for (KeyCacheEntry* e : g_kc) {
+        if (e->dev != dev || e->alg != alg || e->kind != kind || e->sig != sig) continue;
+        if (e->sid != sid || s == hipStreamPerThread) {
+            if (hipEventQuery(e->ready) != hipSuccess) {
+                (void)hipGetLastError();
+                LCB_TRY(hipStreamWaitEvent(s, e->ready, 0));
+            }
+        }
+        *out = e->kt;
+        return 0;
+    }
+    const size_t nkeys = klen.size();
+    const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = (nkeys * 4 + 15) & ~(size_t)15;
+    const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
+    // One host image of [key bytes | offsets | lengths] and ONE copy.
+    std::vector<uint8_t> img(blob_b + 2 * tab_b, 0);
+    if (!blob.empty()) memcpy(img.data(), blob.data(), blob.size());
+    memcpy(img.data() + blob_b, koff.data(), nkeys * 4);
+    memcpy(img.data() + blob_b + tab_b, klen.data(), nkeys * 4);
+    const bool cache = g_kc.size() < kKeyCacheMax;
+    uint8_t* dbuf = nullptr;
+    if (cache) {
+        LCB_TRY(hipMalloc(reinterpret_cast<void**>(&dbuf), img.size() + mid_b));
+    } else {
+        LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), img.size() + mid_b, s));
+        *temp = dbuf;
+    }
+    // Pageable source: the copy returns once the bytes are staged, so the
+    // host image may die on return.
+    hipError_t e = hipMemcpyAsync(dbuf, img.data(), img.size(), hipMemcpyHostToDevice, s);
+    KeyTable kt;
+    kt.mode = (uint32_t)kind;
+    kt.keys = dbuf;
+    kt.key_off = reinterpret_cast<const uint32_t*>(dbuf + blob_b);
+    kt.key_len = reinterpret_cast<const uint32_t*>(dbuf + blob_b + tab_b);
+    kt.nkeys = (uint32_t)nkeys;
+    kt.mid = reinterpret_cast<const uint32_t*>(dbuf + blob_b + 2 * tab_b);
+    if (e == hipSuccess) {
+        if (kind == 0) {
+            // One HMAC key: the key block by value (short key) or H(key) of the
+            // uploaded bytes (long key), as hmac_setup always did.
+            launch_hmac_prep(alg, *kb, blob.size() > bsize(alg) ? dbuf : nullptr, blob.size(),
+                             const_cast<uint32_t*>(kt.mid), s);
+        } else if (kind != LCB_HASH_KEY_SUFFIX) {
+            KArgs a;
+            a.key_mode = kt.mode; a.keys = kt.keys; a.key_off = kt.key_off; a.key_len = kt.key_len;
+            a.nkeys = kt.nkeys;
+            launch_key_prep(alg, a, const_cast<uint32_t*>(kt.mid), s);
+        }
+        e = hipGetLastError();
+    }
+    hipEvent_t ready = nullptr;
+    if (e == hipSuccess && cache) {
+        e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ready, s);
+    }
+    if (e != hipSuccess) {
+        if (ready) (void)hipEventDestroy(ready);
+        if (cache) (void)hipFree(dbuf);
+        else (void)scratch_free(dbuf, s);
+        *temp = nullptr;
+        return map_err(e);
+    }
+    if (cache) {
+        KeyCacheEntry* ce = new KeyCacheEntry();
+        ce->dev = dev; ce->alg = alg; ce->kind = kind; ce->sig.swap(sig);
+        ce->dbuf = dbuf; ce->kt = kt; ce->ready = ready; ce->sid = sid;
+        g_kc.push_back(ce);
+    }
+    *out = kt;
+    return 0;
+}
+
+// HMAC mid-states of one key on `s` (cached, see key_table).  *temp: a
+// per-call buffer to scratch_free after the batch, or null.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid, uint8_t** temp) {
     KeyBlock kb;
     memset(&kb, 0, sizeof(kb));
-    uint8_t* dkey = nullptr;
-    const size_t B = bsize(alg);
-    if (key_len <= B) {
-        if (key_len) memcpy(kb.w, key, key_len);
-    } else {
-        // Long key: hashed on the device.  The copy is waited for so the
-        // caller may release `key` on return (pageable source memory).
-        LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dkey), key_len, s));
-        LCB_TRY(hipMemcpyAsync(dkey, key, key_len, hipMemcpyHostToDevice, s));
-        LCB_TRY(hipStreamSynchronize(s));
-    }
-    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(mid), 2 * kMidWords * sizeof(uint32_t), s));
-    launch_hmac_prep(alg, kb, dkey, key_len, *mid, s);
-    LCB_TRY(hipGetLastError());
-    *dkey_out = dkey;
+    if (key_len <= bsize(alg) && key_len) memcpy(kb.w, key, key_len);
+    std::vector<uint8_t> blob(key, key + key_len);
+    std::vector<uint32_t> koff(1, 0u), klen(1, (uint32_t)key_len);
+    if (key_len > UINT32_MAX) return EINVAL;
+    KeyTable kt;
+    const int rc = key_table(alg, 0, blob, koff, klen, &kb, s, &kt, temp);
+    if (rc) return rc;
+    *mid = kt.mid;
     return 0;
 }
 
 // Launch the batch kernel, bucketing a large ragged batch by length first
-// (stream-ordered temporaries, no synchronisation).
+// (no synchronisation).  Bucketing scratch: work_buf, else the stream's
+// scratch (ss, held by the caller), else a stream-ordered allocation.
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     uint32_t* work = nullptr;
     // The bucketing permutation holds message indices as uint32 and, padded
     // per key to whole tiles, up to 63 pad entries (kOrderPad = 2^32 - 1) per
     // key: its length, the scan and the tile count must stay below 2^32.
     if (a.lengths && a.order == nullptr && a.count >= kBucketMaxCount) return EINVAL;
+    bool pooled = false;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
         // work: [key totals | spare | spare | entry count | order | ...]
         const size_t bytes = bucket_words(a.count) * sizeof(uint32_t);
@@ -129,6 +353,7 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
             work = work_buf;
         } else {
             LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&work), bytes, s));
+            pooled = true;
         }
         const bool tiles = tiles_take(alg, a);
         launch_bucketing(a, work, work + kBucketWork, tiles, s);
@@ -137,8 +362,15 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();
-    if (work && work != work_buf) (void)scratch_free(work, s);
+    if (pooled) (void)scratch_free(work, s);
     return map_err(e);
+}
+
+// Bucketing scratch words of a batch (0: not bucketed).
+static size_t ordered_words(const KArgs& a) {
+    return (a.lengths && a.order == nullptr && a.count >= kBucketMinCount && a.count < kBucketMaxCount)
+               ? bucket_words(a.count)
+               : 0;
 }
 
 int device_cu_count() {
@@ -208,23 +440,36 @@ static void set_keys(KArgs& a, const KeyTable* kt, const uint32_t* index) {
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                  uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init,
-                 const KeyTable* kt) {
+                 const KeyTable* kt, const KeyCheck* kc) {
     KArgs a;
     a.data = data; a.offsets = offsets; a.lengths = lengths; a.order = nullptr;
     a.count = count; a.stride = stride; a.fixed_len = fixed_len; a.digests = digests;
     a.mid = nullptr;
     a.init = init;
     set_keys(a, kt, kt ? kt->index : nullptr);
-    uint32_t* mid = nullptr;
-    uint8_t* dkey = nullptr;
+    if (kc) {
+        a.bad = kc->dflag;
+        a.bad_epoch = kc->epoch;
+    }
+    uint8_t* temp = nullptr;
     if (key) {
-        int rc = hmac_setup(alg, key, key_len, s, &mid, &dkey);
+        const uint32_t* mid = nullptr;
+        int rc = hmac_setup(alg, key, key_len, s, &mid, &temp);
         if (rc) return rc;
         a.mid = mid;
     }
-    int rc = launch_ordered(alg, a, s);
-    if (mid) (void)scratch_free(mid, s);
-    if (dkey) (void)scratch_free(dkey, s);
+    int rc;
+    const size_t words = ordered_words(a);
+    if (kc && kc->work_words >= words) {
+        rc = launch_ordered(alg, a, s, kc->work);   // the keyed call's stream scratch
+    } else if (words) {
+        StreamScratch* ss = stream_scratch_acquire(s, words * sizeof(uint32_t));
+        rc = launch_ordered(alg, a, s, ss ? reinterpret_cast<uint32_t*>(stream_scratch_payload(ss)) : nullptr);
+        stream_scratch_release(ss);
+    } else {
+        rc = launch_ordered(alg, a, s);
+    }
+    if (temp) (void)scratch_free(temp, s);
     return rc;
 }
 
@@ -346,10 +591,10 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     const bool src_pinned = is_pinned(data);
     const bool dig_pinned = is_pinned(digests);
 
-    uint32_t* mid = nullptr;
-    uint8_t* dkey = nullptr;
+    const uint32_t* mid = nullptr;
+    uint8_t* temp = nullptr;
     if (key) {
-        rc = hmac_setup(alg, key, key_len, S.st[0], &mid, &dkey);
+        rc = hmac_setup(alg, key, key_len, S.st[0], &mid, &temp);
         if (rc) return rc;
         LCB_TRY(hipStreamSynchronize(S.st[0]));   // mid-states visible to both streams
     }
@@ -458,9 +703,8 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     }
     int rc2 = drain(0);
     int rc3 = drain(1);
-    if (mid || dkey) {  // both streams are drained: release the HMAC state
-        if (mid) (void)scratch_free(mid, S.st[0]);
-        if (dkey) (void)scratch_free(dkey, S.st[0]);
+    if (temp) {  // both streams are drained: release a per-call HMAC state
+        (void)scratch_free(temp, S.st[0]);
         (void)hipStreamSynchronize(S.st[0]);
     }
     if (rc) return rc;
@@ -545,55 +789,107 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     for (size_t k = 0; k < nkeys; ++k)
         if (klen[k]) memcpy(blob.data() + koff[k], keys + (key_offsets ? key_offsets[k] : 0), klen[k]);
     hipStream_t s = dev_mode ? reinterpret_cast<hipStream_t>(stream) : nullptr;
-    const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = nkeys * 4;
-    const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
-    uint8_t* dbuf = nullptr;
-    // [key bytes | key offsets | key lengths | mid-states | bad-index word]
-    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), blob_b + 2 * tab_b + mid_b + 16, s));
-    uint32_t* d_bad = reinterpret_cast<uint32_t*>(dbuf + blob_b + 2 * tab_b + mid_b);
-    uint32_t h_bad = 0;
+    // The device key table (bytes, offsets, lengths, mid-states): cached
+    // across calls with the same keys (key_table), else built on `s`.
     KeyTable kt;
-    kt.mode = (uint32_t)key_mode;
-    kt.keys = dbuf;
-    kt.key_off = reinterpret_cast<const uint32_t*>(dbuf + blob_b);
-    kt.key_len = reinterpret_cast<const uint32_t*>(dbuf + blob_b + tab_b);
-    kt.nkeys = (uint32_t)nkeys;
-    kt.mid = reinterpret_cast<const uint32_t*>(dbuf + blob_b + 2 * tab_b);
+    uint8_t* temp = nullptr;
+    int rc = key_table(alg, key_mode, blob, koff, klen, nullptr, s, &kt, &temp);
+    if (rc) return rc;
     kt.index = key_index;
-    int rc = 0;
-    // The table's host vectors die on return: copy, then wait for the copies.
-    if (hipMemcpyAsync(dbuf, blob.data(), blob.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dbuf + blob_b, koff.data(), tab_b, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dbuf + blob_b + tab_b, klen.data(), tab_b, hipMemcpyHostToDevice, s) != hipSuccess)
-        rc = EIO;
-    if (!rc && key_mode != LCB_HASH_KEY_SUFFIX) {
-        KArgs a;
-        a.key_mode = kt.mode; a.keys = kt.keys; a.key_off = kt.key_off; a.key_len = kt.key_len; a.nkeys = kt.nkeys;
-        launch_key_prep(alg, a, const_cast<uint32_t*>(kt.mid), s);
+    if (!dev_mode) {
+        // Host mode: the pipeline's own streams read the table; wait for it.
+        rc = hipStreamSynchronize(s) == hipSuccess ? 0 : EIO;
+        if (!rc) rc = batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
+                                 nullptr, nullptr, &kt);
+        if (temp) (void)scratch_free(temp, s);
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    if (!key_index) {
+        rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr,
+                          &kt);
+        if (temp) (void)scratch_free(temp, s);
+        return rc;
+    }
+    // Device mode with per-message key indices: an index >= nkeys is EINVAL
+    // and no digest is written, as in host mode.  The check kernel runs
+    // first: a block that finds a bad index writes this call's epoch into
+    // the stream scratch's flag word, and the last of its blocks (a counter
+    // in the same header) writes epoch | bad bit into a pinned host word.
+    // The batch is enqueued right behind the check with every digest store
+    // gated on the device flag (batch_aborted); only then does the host wait,
+    // for the check's host word, not for the batch.  The GPU never idles for
+    // the host's round trip, and nothing is recorded on the stream (r4: three
+    // key uploads, a memset, a read-back and 40 us of idle stream per keyed
+    // call; an event record costs 6.5 us: profiles/r5_pkt_gaps.txt).
+    KArgs probe;
+    probe.lengths = lengths; probe.order = nullptr; probe.count = count;
+    const size_t words = ordered_words(probe);
+    StreamScratch* ss = stream_scratch_acquire(s, std::max<size_t>(words, 1) * sizeof(uint32_t));
+    if (ss) {
+        ss->epoch = (ss->epoch + 1) & 0x7fffffffu;
+        if (ss->epoch == 0) ss->epoch = 1;
+        KeyCheck kc;
+        kc.dflag = reinterpret_cast<const uint32_t*>(ss->p);
+        kc.epoch = ss->epoch;
+        kc.work = reinterpret_cast<uint32_t*>(stream_scratch_payload(ss));
+        kc.work_words = ss->bytes / sizeof(uint32_t);
+        const uint32_t nblk = launch_key_check(key_index, count, (uint32_t)nkeys, reinterpret_cast<uint32_t*>(ss->p),
+                                               ss->hflag, kc.epoch, ss->ctr, s);
+        ss->ctr += nblk;
         rc = map_err(hipGetLastError());
-    }
-    // Device mode: an out-of-range key index is found on the device before
-    // the batch runs and read back at the sync the key upload needs anyway:
-    // EINVAL and no digest written, as in host mode.
-    if (!rc && dev_mode && key_index) {
-        if (hipMemsetAsync(d_bad, 0, 4, s) != hipSuccess) rc = EIO;
+        if (!rc)
+            rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr,
+                              &kt, &kc);
+        if (temp) (void)scratch_free(temp, s);
         if (!rc) {
-            launch_key_check(key_index, count, (uint32_t)nkeys, d_bad, s);
-            if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(&h_bad, d_bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
-                rc = EIO;
+            // Spin on the host word for a while, then poll with short sleeps;
+            // a stream that has drained without the word is an error.
+            for (uint64_t it = 0;; ++it) {
+                const uint32_t v = __atomic_load_n(ss->hflag, __ATOMIC_ACQUIRE);
+                if ((v & 0x7fffffffu) == kc.epoch) {
+                    if (v >> 31) rc = EINVAL;
+                    break;
+                }
+                if (it < 20000) {
+                    __builtin_ia32_pause();
+                    continue;
+                }
+                if ((it & 63) == 0) {
+                    const hipError_t q = hipStreamQuery(s);
+                    if (q == hipSuccess &&
+                        (__atomic_load_n(ss->hflag, __ATOMIC_ACQUIRE) & 0x7fffffffu) != kc.epoch) {
+                        rc = EIO;
+                        break;
+                    }
+                    if (q != hipSuccess && q != hipErrorNotReady) {
+                        rc = map_err(q);
+                        break;
+                    }
+                    (void)hipGetLastError();
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(5));
+            }
         }
+        stream_scratch_release(ss);   // held until the host word was read (epochs are per buffer)
+        return rc;
     }
-    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EIO;
-    if (!rc && h_bad) rc = EINVAL;
+    // No stream scratch free (another thread enqueues on this stream): the
+    // check's flag in a pooled word, read back before the batch.
+    uint32_t* d_bad = nullptr;
+    uint32_t h_bad = 0;
+    if (scratch_alloc(reinterpret_cast<void**>(&d_bad), 16, s) != hipSuccess) rc = ENOMEM;
+    if (!rc && hipMemsetAsync(d_bad, 0, 4, s) != hipSuccess) rc = EIO;
     if (!rc) {
-        rc = dev_mode ? batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s,
-                                     nullptr, &kt)
-                      : batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
-                                   nullptr, nullptr, &kt);
+        (void)launch_key_check(key_index, count, (uint32_t)nkeys, d_bad, nullptr, 1u, 0u, s);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h_bad, d_bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = EIO;
     }
-    (void)scratch_free(dbuf, s);
-    if (!dev_mode) (void)hipStreamSynchronize(s);
+    if (!rc && h_bad) rc = EINVAL;
+    if (!rc) rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr, &kt);
+    if (d_bad) (void)scratch_free(d_bad, s);
+    if (temp) (void)scratch_free(temp, s);
     return rc;
 }
 

@@ -611,17 +611,16 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
     if (!rc && key) {
         // HMAC mid-states once per queue (the key is fixed for its lifetime).
         hipStream_t st = q->slots[0].stream;
-        uint32_t* mid = nullptr;
-        uint8_t* dkey = nullptr;
-        rc = hmac_setup(alg, key, key_len, st, &mid, &dkey);
+        const uint32_t* mid = nullptr;
+        uint8_t* temp = nullptr;
+        rc = hmac_setup(alg, key, key_len, st, &mid, &temp);
         if (!rc) {
             uint32_t* keep = nullptr;
             if (hipMalloc(reinterpret_cast<void**>(&keep), 2 * kMidWords * sizeof(uint32_t)) != hipSuccess ||
                 hipMemcpyAsync(keep, mid, 2 * kMidWords * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) !=
                     hipSuccess)
                 rc = ENOMEM;
-            (void)scratch_free(mid, st);
-            if (dkey) (void)scratch_free(dkey, st);
+            if (temp) (void)scratch_free(temp, st);
             if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = EIO;
             q->mid = keep;
         }

@@ -30,7 +30,18 @@ struct KArgs {
     const uint32_t* key_off = nullptr;
     const uint32_t* key_len = nullptr;
     uint32_t nkeys = 0;
+    // Keyed device batches: the key-index check's flag word; a digest is
+    // stored only while *bad != bad_epoch (batch_aborted).
+    const uint32_t* bad = nullptr;
+    uint32_t bad_epoch = 0;
 };
+
+// True when the key-index check of this keyed batch found an index >= nkeys
+// (lcb_hash_batch_keyed, device mode): its kernels then store no digest.
+__device__ __forceinline__ bool batch_aborted(const KArgs& a) {
+    if (!a.bad) return false;
+    return *(const __attribute__((address_space(1))) uint32_t*)(uintptr_t)a.bad == a.bad_epoch;
+}
 
 // KArgs::key_mode.  kKeyNone: plain digest, or single-key HMAC when mid is
 // set (lcb_hash_batch).  The others take key k = key_index[i]:
@@ -166,7 +177,12 @@ void launch_hmac_prep(int alg, const KeyBlock& kb, const uint8_t* dkey, uint64_t
 void launch_key_prep(int alg, const KArgs& a, uint32_t* mid, hipStream_t s);
 void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStream_t s);
 // *bad |= 1 if any of idx[0..count) >= nkeys (bad zeroed by the caller).
-void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, hipStream_t s);
+// bad[0] = epoch if any of idx[0..count) >= nkeys.  With a pinned host word
+// hbad: bad[1] counts the kernel's finished blocks (it holds ctr before the
+// launch) and the last block writes epoch | (bad ? 1 << 31 : 0) to *hbad.
+// Returns the kernel's block count (the host adds it to its ctr).
+uint32_t launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, uint32_t* hbad,
+                          uint32_t epoch, uint32_t ctr, hipStream_t s);
 // HBM read probes (lcb_hash_gpu_read_probe): mode 0 = the fixed-stride line
 // stream alone over `a`'s records, mode 1 = linear coalesced read of
 // count * stride bytes; sink: one uint32 per record (0) / per thread (1).
@@ -189,10 +205,11 @@ int device_cu_count();                  // compute units of the current device (
 // (the ingestion queue's slots).  Memory stays in the pool.
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 hipError_t scratch_free(void* p, hipStream_t s);
-// Enqueue the HMAC mid-state prep; *mid / *dkey are scratch allocations
-// the caller releases with scratch_free after their last use.
-int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, uint32_t** mid,
-               uint8_t** dkey_out);
+// HMAC mid-states of one key, prepared on `s` and cached by the key's bytes
+// (lcb_hash_gpu.cpp key_table); *temp = a per-call buffer (cache full) the
+// caller releases with scratch_free after its last use, else null.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid,
+               uint8_t** temp);
 // Batch kernel launch, bucketing a large ragged batch by length first.
 // work_buf: optional caller-owned device buffer of bucket_words(count)
 // uint32 for the bucketing of a ragged batch; null = stream-ordered allocation.
@@ -214,10 +231,19 @@ struct KeyTable {
     const uint32_t* mid = nullptr;     // device: 2 * kMidWords words per key
     const uint32_t* index = nullptr;   // per message (device or host memory, as the batch), or nullptr
 };
+// Key-index check of a keyed device batch (lcb_hash_batch_keyed): the flag
+// word the check kernel sets to `epoch`, and the stream scratch the call
+// holds (bucketing work words, reused by the batch).
+struct KeyCheck {
+    const uint32_t* dflag = nullptr;
+    uint32_t epoch = 0;
+    uint32_t* work = nullptr;
+    size_t work_words = 0;
+};
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                  uint32_t fixed_len, uint8_t* digests, hipStream_t s, const uint32_t* init,
-                 const KeyTable* kt = nullptr);
+                 const KeyTable* kt = nullptr, const KeyCheck* kc = nullptr);
 int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,
                uint32_t fixed_len, uint8_t* digests, const uint32_t* init, Stage* stage,

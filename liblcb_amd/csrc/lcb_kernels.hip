@@ -346,22 +346,40 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tile
     default: break;                                               \
     }
 
-// Keyed batches, device mode: flags an out-of-range key index before the
-// batch runs (lcb_hash_batch_keyed returns EINVAL then and writes no digest,
-// as host mode does).  One global atomic OR per offending lane.
+// Keyed batches, device mode: flags an out-of-range key index (lcb_hash_batch_keyed
+// returns EINVAL then and no digest is written, as in host mode).  The flag
+// takes the call's epoch, so it needs no clearing between calls; it gates
+// the batch's digest stores (batch_aborted).  With a host word: every block
+// counts itself in bad[1] (agent-scope acq_rel add: the last block sees
+// every earlier block's flag store), and the last one writes the result to
+// the pinned host word with a system-scope store -- the host polls that word
+// instead of recording an event (6.5 us of stream time each).
 __global__ __launch_bounds__(256) void key_index_check_kernel(const uint32_t* idx, uint64_t count, uint32_t nkeys,
-                                                              uint32_t* bad) {
+                                                              uint32_t* bad, uint32_t* hbad, uint32_t epoch,
+                                                              uint32_t target) {
+    bool any = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (uint64_t)gridDim.x * blockDim.x)
-        if (gptr(idx)[i] >= nkeys) __hip_atomic_fetch_or(gptr(bad), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        any |= gptr(idx)[i] >= nkeys;
+    any = __syncthreads_or(any);
+    if (threadIdx.x != 0) return;
+    if (any) __hip_atomic_store(gptr(bad), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!hbad) return;
+    const uint32_t done = __hip_atomic_fetch_add(gptr(bad) + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (done != target) return;
+    const uint32_t b = __hip_atomic_load(gptr(bad), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hbad, epoch | (b == epoch ? 0x80000000u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-void launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, hipStream_t s) {
+uint32_t launch_key_check(const uint32_t* idx, uint64_t count, uint32_t nkeys, uint32_t* bad, uint32_t* hbad,
+                          uint32_t epoch, uint32_t ctr, hipStream_t s) {
     uint64_t blocks = (count + 255) / 256;
     const uint64_t cap = (uint64_t)4 * device_cu_count();
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(key_index_check_kernel, dim3((unsigned)(blocks ? blocks : 1)), dim3(256), 0, s, idx, count,
-                       nkeys, bad);
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(key_index_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, idx, count, nkeys, bad, hbad,
+                       epoch, ctr + (uint32_t)blocks);
+    return (uint32_t)blocks;
 }
 
 // The hashes with a tile kernel (kTileOcc > 0): MD5, SHA-1, SHA-224/256.

@@ -475,6 +475,7 @@ __global__ __launch_bounds__(256, H::kBlock == 128 ? 3 : (H::kOcc < 4 ? H::kOcc 
         md_message2(st, msg, len, K, kl, 0);
         st.digest_words(dw);
     }
+    if (batch_aborted(a)) return;
     store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
 }
 

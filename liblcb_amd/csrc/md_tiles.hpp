@@ -113,11 +113,22 @@ __device__ __forceinline__ void tile_shift(const uint32_t* c, const uint32_t* y,
 }
 // The carry block's first 16 words: word j of the lane's rotated stream is
 // still the carry (dwords 16..31 of line L - 1) while its chunk j >> 2 + m
-// lies below 4, else it wrapped round into line L (y[16 + j]).
-__device__ __forceinline__ void tile_merge(uint32_t* c, const uint32_t* y, uint32_t m) {
+// lies below 4, else it wrapped round into line L (y[16 + j]).  Chunk 0 is
+// always kept (m <= 3); the three keep masks of chunks 1..3 (m < 3, m < 2,
+// m < 1) are lane masks computed once per tile (TileKeep): 12 v_cndmask per
+// line and no per-line compares.
+struct TileKeep {
+    bool k1, k2, k3;
+    __device__ __forceinline__ void init(uint32_t m) {
+        k1 = m < 3u;
+        k2 = m < 2u;
+        k3 = m < 1u;
+    }
+};
+__device__ __forceinline__ void tile_merge(uint32_t* c, const uint32_t* y, const TileKeep& kp) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const bool keep = (uint32_t)q + m < 4u;
+    for (int q = 1; q < 4; ++q) {
+        const bool keep = q == 1 ? kp.k1 : (q == 2 ? kp.k2 : kp.k3);
 #pragma unroll
         for (int i = 0; i < 4; ++i) c[4 * q + i] = keep ? c[4 * q + i] : y[16 + 4 * q + i];
     }
@@ -202,7 +213,9 @@ __device__ __forceinline__ void tile_finish(const KArgs& a, H& st, const TileRec
         md_outer(o, dw);
         o.digest_words(dw);
     }
-    if (r.valid) store_digest<H::kDigest>(a.digests + (uint64_t)r.idx * H::kDigest, dw);
+    bool store = r.valid;
+    if constexpr (kMode == kTileKeyedHmac || kMode == kTileKeyedSuffix) store = store && !batch_aborted(a);
+    if (store) store_digest<H::kDigest>(a.digests + (uint64_t)r.idx * H::kDigest, dw);
 }
 
 template <class H, int kMode>
@@ -285,11 +298,15 @@ __device__ __forceinline__ uint32_t group8_or(uint32_t v) {
 // 8 KiB slab with 8 global_load_lds_dwordx4.  Lane group q (lanes 8q ..
 // 8q + 7) carries, in instruction g, the whole 128-B cache line L of record
 // j = 8q + g (one of its own lanes' records), lane 8q + c the record's chunk
-// (c ^ g) + m_j (mod 8; m_j: record j's chunk rotation): the texture unit
-// sees 8 whole cache lines per instruction.  Instruction g lands at slab row
-// 8g + q, so record j's line is row R(j) = 8 (j & 7) + (j >> 3), its rotated
-// chunk k in slot k ^ (j & 7): the 16 lanes of a ds_read_b128 group hit 16
-// different bank groups.  Addressing: the saddr form, a wave-uniform scalar
+// c + m_j (mod 8; m_j: record j's chunk rotation): the texture unit sees 8
+// whole cache lines per instruction.  Instruction g lands at slab + g * kRow
+// (kRow = 1,040: 1 KiB plus one 16-B slot), so record j's row starts at
+// (j & 7) * 1040 + (j >> 3) * 128, in bank group ((j & 7) + 8 (j >> 3)) mod 16,
+// and its rotated chunk k is the row's slot k: the 16 lanes of every
+// ds_read_b128 group start in 16 different bank groups, and take() reads
+// the 8 chunks at one base plus immediate offsets (no per-chunk address
+// VALU; the XOR-swizzled rows of 8 KiB slabs took 8 v_xor per line).
+// Addressing: the saddr form, a wave-uniform scalar
 // base (the tile's lowest stream base + 128 L) plus one 32-bit offset per
 // instruction (8 VGPRs; md_tile_stream checks that the tile spans less than
 // 4 GiB).  In the last lines (masked) a chunk past its record's last byte is
@@ -300,6 +317,11 @@ __device__ __forceinline__ uint32_t group8_or(uint32_t v) {
 #ifndef LCB_TILE_SKIP
 #define LCB_TILE_SKIP 1
 #endif
+#ifndef LCB_TILE_ROW
+#define LCB_TILE_ROW 1040
+#endif
+constexpr uint32_t kTileRow = LCB_TILE_ROW;             // LDS bytes per DMA instruction (padded)
+constexpr uint32_t kTileSlab = 7 * kTileRow + 1024;     // one wave's slab
 struct TileGatherStream {
     uint8_t* slab;
     uint32_t lane;
@@ -319,7 +341,7 @@ struct TileGatherStream {
         for (int g = 0; g < 8; ++g) {
             const uint32_t rj = (uint32_t)__shfl((int)rel, (int)(ln & ~7u) + g, 64);
             const uint32_t mj = (mpk >> (2 * g)) & 3u;
-            voff[g] = rj + ((((ln & 7u) ^ (uint32_t)g) + mj) & 7u) * 16u;
+            voff[g] = rj + (((ln & 7u) + mj) & 7u) * 16u;
         }
     }
     __device__ __forceinline__ void issue(uint32_t L) {
@@ -331,7 +353,7 @@ struct TileGatherStream {
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g]),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             (__attribute__((address_space(3))) void*)(slab + g * kTileRow), 16, 0,
                                              kLdsAux);
     }
     // lastc: index of this lane's last stream chunk holding a record byte;
@@ -351,7 +373,7 @@ struct TileGatherStream {
 #endif
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint32_t k = (((ln & 7u) ^ (uint32_t)g) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
+            const uint32_t k = ((ln & 7u) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
 #if LCB_TILE_SKIP
             // Only the chunks that hold record bytes are fetched: a lane whose
             // chunk lies past its record's last byte (or, in line 0, before
@@ -373,12 +395,12 @@ struct TileGatherStream {
 #endif
             if (any)
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
-                                                 (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                                 (__attribute__((address_space(3))) void*)(slab + g * kTileRow), 16, 0,
                                                  kLdsAux);
 #else
             const uint32_t v = k < ((nv >> (4 * g)) & 15u) ? voff[g] + L * 128u : voff[g] - 16u * k;
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             (__attribute__((address_space(3))) void*)(slab + g * kTileRow), 16, 0,
                                              kLdsAux);
 #endif
         }
@@ -389,12 +411,13 @@ struct TileGatherStream {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         using lds_cu4 = __attribute__((address_space(3))) const v4u;
-        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) +
-                     (8u * (lane & 7u) + (lane >> 3)) * 128u + (lane & 7u) * 16u;
-        asm volatile("" : "+v"(b));
+        // The row base (one VGPR); the 8 chunks at immediate offsets.
+        const uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) +
+                           (lane & 7u) * kTileRow + (lane >> 3) * 128u;
+        lds_cu4* row = (lds_cu4*)(uintptr_t)b;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const v4u v = *(lds_cu4*)(uintptr_t)(b ^ (uint32_t)(k << 4));
+            const v4u v = row[k];
             y[4 * k] = v.x; y[4 * k + 1] = v.y; y[4 * k + 2] = v.z; y[4 * k + 3] = v.w;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -496,28 +519,59 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     };
     const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
     if (kMode == kTileKeyedSuffix && LE) issue(0);
+    TileKeep kp;      // the merge's keep masks (lane masks, once per tile)
+    kp.init(m);
     uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
     // Whole-block lines: both blocks of line L (2L - 1 - h and 2L - h) are
-    // whole message blocks of every lane.
+    // whole message blocks of every lane.  Two line buffers in turn, the
+    // loop unrolled by two so that which buffer holds the carry is fixed at
+    // compile time: line L lands in one buffer while the other's upper half
+    // (dwords 16..31 of line L - 1) is the carry, merged in place -- no
+    // per-line copy of the carry (16 v_mov per line before).
     uint32_t L = 0;
-    for (; L < LF; ++L) {
-        uint32_t y[32];
+    if (LF) {
+        uint32_t ya[32], yb[32];
+        // Line L into y, cr = the other buffer's upper half (the carry).
+        auto whole_line = [&](uint32_t Ln, uint32_t* y, uint32_t* cr) {
 #if LCB_TILE_PRIO
-        if ((L & 15u) == 0) tile_prio(NL - L);
+            if ((Ln & 15u) == 0) tile_prio(NL - Ln);
 #endif
-        ls.take(y);
-        LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
-        if (L + 1 < LE) issue(L + 1);
-        uint32_t w[16];
-        if (L > 0) {   // block 2L - 1 - h: the carry merged with this line's wrapped chunks
-            if (rotated) tile_merge(c, y, rot());
-            tile_shift<kR, kA16>(c, y, sh, w);
+            ls.take(y);
+            LCB_TRACE(if (Ln + 1 == NL) tr.mark(3);)
+            if (Ln + 1 < LE) issue(Ln + 1);
+            uint32_t w[16];
+            // block 2L - 1 - h: the carry merged with this line's wrapped chunks
+            if (rotated) tile_merge(cr, y, kp);
+            tile_shift<kR, kA16>(cr, y, sh, w);
             tile_compress(st, w);
+            tile_shift<kR, kA16>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
+            tile_compress(st, w);
+        };
+        {   // line 0: no carry block; its own block only when the record starts in the first half
+#if LCB_TILE_PRIO
+            tile_prio(NL);
+#endif
+            ls.take(ya);
+            LCB_TRACE(tr.mark(2); if (NL == 1) tr.mark(3);)
+            if (1 < LE) issue(1);
+            uint32_t w[16];
+            tile_shift<kR, kA16>(ya, ya + 16, sh, w);
+            if (half() == 0) tile_compress(st, w);
         }
-        tile_shift<kR, kA16>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
-        if (L > 0 || half() == 0) tile_compress(st, w);
+        L = 1;
+        for (; L + 1 < LF; L += 2) {
+            whole_line(L, yb, ya + 16);
+            whole_line(L + 1, ya, yb + 16);
+        }
+        if (L < LF) {
+            whole_line(L, yb, ya + 16);
+            ++L;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+            for (int k = 0; k < 16; ++k) c[k] = yb[16 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = ya[16 + k];
+        }
     }
     if constexpr (kMode == kTileKeyedSuffix) {
         const uint32_t nd = LF ? 2u * LF - 1u - half() : 0u;       // blocks 0 .. nd - 1 done
@@ -541,7 +595,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         }
         uint32_t w[16];
         if (L > 0) {
-            if (rotated) tile_merge(c, y, rot());
+            if (rotated) tile_merge(c, y, kp);
             tile_shift<kR, kA16>(c, y, sh, w);
             tile_block<H, kMode>(st, 2 * L - 1 - half(), w, len, m_, nblk, 2 * L - 1 < NF);
         }
@@ -565,7 +619,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 // profiles/r4_tile_np_ab.txt).
 template <class H, int kMode>
 __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kTileSlab];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t t = blockIdx.x;
     // The entry count and the tile's `order` entries load together (`order`

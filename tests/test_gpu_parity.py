@@ -503,3 +503,36 @@ def test_ragged_every_line_phase(gpu, oracle, shape, alg):
         got = gpu.hash_batch_keyed(alg, mode, keys, dd, key_index=dev(kidx, np.int32), offsets=do,
                                    lengths=dl).cpu().numpy()
         assert np.array_equal(got, exp), (shape, mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_tiles_pad_heavy(gpu, oracle, mode):
+    """Regression for the round-4 fault (a readfirstlane under
+    a per-lane select read a pad entry): tiles whose lanes 1..63 are pads
+    (a key with ONE record), and a key run of 64k + 1 records (its last
+    tile: 1 record + 63 pads), in plain, keyed-HMAC and keyed-suffix form,
+    vs the oracle."""
+    import torch
+    from tests.test_radius_gpu import KEYS
+    n = 4097 + 3
+    lens = np.full(n, 100, np.uint32)
+    lens[17] = 1000                 # a key of its own (class 16)
+    lens[2222] = 3000               # another lone record (class 47)
+    lens[4000] = 65                 # class 2, alone at its phase below
+    offs = np.arange(n, dtype=np.uint64) * 3072 + 16
+    offs[4000] += 4                 # dword phase 1: a one-record key
+    data = gen_stream(0xBAD0, int(offs[-1]) + 3072)
+    dd = torch.as_tensor(data, device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    kidx = (np.arange(n) % len(KEYS)).astype(np.uint32)
+    for alg in (1, 2, 4):
+        if mode == 0:
+            got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl).cpu().numpy()
+            exp = oracle.batch(alg, data, offs, lens)
+        else:
+            got = gpu.hash_batch_keyed(alg, mode, KEYS, dd, key_index=torch.as_tensor(kidx.astype(np.int32),
+                                       device="cuda"), offsets=do, lengths=dl).cpu().numpy()
+            exp = oracle.batch_keyed(alg, mode, KEYS, data, kidx, offs, lens)
+        assert np.array_equal(got, exp), (alg, mode)

@@ -341,3 +341,58 @@ def test_wrapper_validation_host():
         liblcb_amd.hash_batch(1, d, offsets=offs, lengths=lens, out=np.empty((n, 15), np.uint8))
     with pytest.raises(ValueError):
         liblcb_amd.hash_batch_multi([0], 1, d, offsets=offs, lengths=lens, copy_parts=True)
+
+
+@pytest.mark.gpu
+def test_keyed_check_epochs_same_stream(gpu, oracle):
+    """The device-mode key-index check writes the call's epoch into the
+    stream scratch's flag word (lcb_hash_gpu.cpp, r5): bad, good, bad, good
+    batches back to back on ONE stream -- every bad one is EINVAL with no
+    digest written, every good one right.  Tile kernel (5000 messages,
+    bucketed), per-lane keyed kernel (KEY_PREFIX) and GOST, and a key table
+    that changes between calls (the key cache must not hand one table's
+    mid-states to another)."""
+    import torch
+    from liblcb_amd._lib import LcbHashError
+    data, offs, lens, kidx = _ragged(77, 5000)
+    dd = torch.as_tensor(data, device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    bad = kidx.copy()
+    bad[4321] = len(KEYS) + 3
+    dk_good = torch.as_tensor(kidx.astype(np.int32), device="cuda")
+    dk_bad = torch.as_tensor(bad.astype(np.int32), device="cuda")
+    keys2 = [k[::-1] + b"x" for k in KEYS]           # a second table, same shape
+    for alg, mode in ((1, 1), (1, 3), (4, 1), (1, 2), (7, 1)):
+        for rep in range(2):
+            for keys in (KEYS, keys2):
+                out = torch.full((len(lens), gpu.DIGEST_SIZE[alg]), 0x5A, dtype=torch.uint8, device="cuda")
+                with pytest.raises(LcbHashError) as e:
+                    gpu.hash_batch_keyed(alg, mode, keys, dd, key_index=dk_bad, offsets=do, lengths=dl, out=out)
+                assert e.value.errno == errno.EINVAL
+                got = gpu.hash_batch_keyed(alg, mode, keys, dd, key_index=dk_good, offsets=do, lengths=dl)
+                assert np.array_equal(got.cpu().numpy(), oracle.batch_keyed(alg, mode, keys, data, kidx, offs, lens)), \
+                    (alg, mode, rep)
+                torch.cuda.synchronize()
+                assert (out.cpu().numpy() == 0x5A).all(), (alg, mode, rep)
+
+
+@pytest.mark.gpu
+def test_hmac_key_cache_distinct_keys(gpu, oracle):
+    """Single-key HMAC mid-states come from the per-device key cache: many
+    different keys (more than the cache holds) and repeats, every result vs
+    the oracle (short, block-sized and long keys)."""
+    import torch
+    n = 300
+    data = gen_stream(91, n * 130)
+    dd = torch.as_tensor(data, device="cuda")
+    offs = np.arange(n, dtype=np.uint64) * 130
+    lens = (np.arange(n) % 129).astype(np.uint32)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    keys = [bytes([i]) * (i * 7 % 150) for i in range(24)]
+    for rep in range(2):
+        for i, k in enumerate(keys):
+            alg = (1, 2, 4, 6, 7)[i % 5]
+            got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=k).cpu().numpy()
+            assert np.array_equal(got, oracle.batch(alg, data, offs, lens, key=k)), (alg, i, rep)

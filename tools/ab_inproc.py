@@ -75,6 +75,7 @@ def main():
     torch.cuda.set_device(0)
     libs = {n: load(n) for n in a.libs.split(",")}
     s = torch.cuda.current_stream()
+    bad = []
     for wname in a.work.split(","):
         count, offs, lens, stride, total = workload(wname)
         data = liblcb_amd.gen_synthetic(0x6C62636861736821, total + 64)
@@ -117,6 +118,11 @@ def main():
                     res[n].append(e0.elapsed_time(e1) / launches)
             out = {"work": wname, "alg": alg_name, "launches": launches, "rounds": a.rounds,
                    "digests_equal": same}
+            if not same:
+                # A faster build with other digests is not a result: mark the
+                # row and fail the run.
+                out["INVALID"] = "digests differ between builds"
+                bad.append((wname, alg_name))
             for n, v in res.items():
                 v = sorted(v)
                 out[n] = {"median_ms": round(v[len(v) // 2], 4), "min_ms": round(v[0], 4),
@@ -128,6 +134,8 @@ def main():
             del dig
         del data, do, dl
         torch.cuda.empty_cache()
+    if bad:
+        raise SystemExit("ab_inproc: digests differ between builds for %s" % bad)
 
 
 if __name__ == "__main__":
