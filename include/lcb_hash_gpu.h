@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define LCB_HASH_GPU_ABI_VERSION	4
+#define LCB_HASH_GPU_ABI_VERSION	5
 
 /* Algorithm ids. */
 #define LCB_HASH_MD5		1	/* md5.h */
@@ -99,11 +99,14 @@ int	lcb_hash_batch(int alg, const uint8_t *key, size_t key_len,
  * keys, key_offsets and key_lengths are HOST memory.  key_index lives where
  * the batch does (device memory with LCB_HASH_F_DEVICE).  Per-key state
  * (HMAC ipad/opad mid-states, the prefix's whole-block state) is computed
- * once per key on the device.  An index >= nkeys is EINVAL in both modes and
- * no digest is written (device mode checks the indices on the device before
- * the batch runs, read back at the key-table sync).  The call waits for the key table
- * upload (the host arrays may be released on return); with
- * LCB_HASH_F_DEVICE the batch itself stays asynchronous on `stream`.
+ * once per key on the device, and kept on the device for later calls with
+ * the same key bytes (a per-device cache of up to 16 tables; HMAC keys of
+ * lcb_hash_batch share it).  An index >= nkeys is EINVAL in both modes and
+ * no digest is written: device mode checks the indices on the device ahead
+ * of the batch and gates every digest store on the result; the call waits
+ * for that check (so for the work already on `stream`), not for the batch,
+ * which stays asynchronous on `stream`.  The host arrays may be released on
+ * return.
  */
 #define LCB_HASH_KEY_HMAC	1
 #define LCB_HASH_KEY_PREFIX	2
@@ -193,7 +196,12 @@ int	gost3411_2012_hmac_get_digest_batch(size_t bits, const uint8_t *key,
  *                           `stream` and required complete inputs).
  * LCB_HASH_F_COPY_PARTS without LCB_HASH_F_DEVICE is EINVAL.
  * With devs = {d} it equals lcb_hash_batch on device d.  Errors: EINVAL,
- * ENODEV (an ordinal out of range), ENOMEM, EIO. */
+ * ENODEV (an ordinal out of range), ENOMEM, EIO.
+ * Device mode enables peer access from every device to devs[0] once
+ * (hipDeviceEnablePeerAccess) and enqueues every remote part's copies
+ * before it waits for any part; part streams and buffers are pooled per
+ * device.  lcb_hash_multi_stats reports what the device-mode calls did
+ * (ABI v5). */
 int	lcb_hash_partition(const uint32_t *lengths, size_t count,
 	    uint32_t fixed_len, size_t nparts, uint64_t *first);
 int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
@@ -201,6 +209,17 @@ int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
 	    const uint64_t *offsets, const uint32_t *lengths, size_t count,
 	    uint64_t stride, uint32_t fixed_len, uint8_t *digests, uint32_t flags,
 	    void *stream);
+typedef struct lcb_hash_multi_stats_s {
+	uint64_t	calls;		/* device-mode lcb_hash_batch_multi calls */
+	uint64_t	remote_parts;	/* parts hashed on a copy (another device, or COPY_PARTS) */
+	uint64_t	parts_enqueued_before_wait; /* remote parts whose copies, batch and
+					 * digest copy-back were all enqueued before the
+					 * call's first wait on any part */
+	uint64_t	peer_enabled;	/* device pairs (d -> devs[0]) with peer access on */
+	uint64_t	peer_unavailable; /* pairs where hipDeviceCanAccessPeer said no:
+					 * the runtime stages their copies */
+} lcb_hash_multi_stats_t;
+int	lcb_hash_multi_stats(lcb_hash_multi_stats_t *out);
 
 /* Synthetic input: writes bytes [start, start+n) of the stream
  * whose u64 word k (little-endian) is mix64(seed ^ k), into device memory. */

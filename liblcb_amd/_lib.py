@@ -63,6 +63,7 @@ SIGNATURES = [
     ("lcb_hash_partition", ctypes.c_int, [c_vp, c_sz, c_u32, c_sz, c_vp]),
     ("lcb_hash_batch_multi", ctypes.c_int,
      [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32, c_vp, c_u32, c_vp]),
+    ("lcb_hash_multi_stats", ctypes.c_int, [c_vp]),
     ("lcb_hash_gen_synthetic", ctypes.c_int, [c_u64, c_u64, c_vp, c_sz, c_vp]),
     ("lcb_hash_gpu_gost_table", ctypes.c_int, [c_vp]),
     ("lcb_hash_gpu_read_probe", ctypes.c_int, [ctypes.c_int, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp]),
@@ -83,6 +84,12 @@ _CHA = [c_vp, c_sz, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_sz, c_u64, c_u32
 CHACHA_SIGNATURES = [("lcb_chacha_batch", ctypes.c_int, [ctypes.c_int] + _CHA),
                      ("chacha_batch", ctypes.c_int, _CHA),
                      ("xchacha_batch", ctypes.c_int, _CHA)]
+
+
+class MultiStats(ctypes.Structure):
+    """lcb_hash_multi_stats_t (include/lcb_hash_gpu.h)."""
+    _fields_ = [(n, c_u64) for n in ("calls", "remote_parts", "parts_enqueued_before_wait", "peer_enabled",
+                                     "peer_unavailable")]
 
 
 class QueueSettings(ctypes.Structure):

@@ -20,6 +20,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -94,46 +96,127 @@ int multi_host(const std::vector<Part>& parts_in, int alg, const uint8_t* key, s
     return 0;
 }
 
-// Per-part device resources of the device-mode path.
-struct DevPart {
+// ------------------------------------------------ device-mode resources
+// Part slots: a persistent non-blocking stream and a growable buffer on one
+// device, pooled across calls (r4 created and destroyed a stream and four
+// buffers per part per call).  A call holds its slots until every part has
+// been waited for, so a slot's buffer is idle whenever it is acquired.
+struct PartSlot {
+    int dev = -1;
     hipStream_t s = nullptr;
-    uint8_t* data = nullptr;   // peer copy of the part's byte span (remote parts)
-    uint64_t* off = nullptr;
-    uint32_t* len = nullptr;
-    uint8_t* dig = nullptr;
+    uint8_t* p = nullptr;
+    size_t bytes = 0;
+    bool busy = false;
 };
+std::mutex g_ps_mu;
+std::vector<PartSlot*> g_ps;
+
+PartSlot* slot_acquire(int dev) {
+    std::lock_guard<std::mutex> lk(g_ps_mu);
+    for (PartSlot* x : g_ps)
+        if (x->dev == dev && !x->busy) {
+            x->busy = true;
+            return x;
+        }
+    PartSlot* x = new PartSlot();
+    x->dev = dev;
+    if (hipStreamCreateWithFlags(&x->s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete x;
+        return nullptr;
+    }
+    x->busy = true;
+    g_ps.push_back(x);
+    return x;
+}
+void slot_release(PartSlot* x) {
+    std::lock_guard<std::mutex> lk(g_ps_mu);
+    x->busy = false;
+}
+// The slot's buffer holds `bytes` (current device = the slot's); the slot is
+// idle (its last use was waited for), so growing frees at once.
+hipError_t slot_reserve(PartSlot* x, size_t bytes) {
+    if (x->bytes >= bytes && x->p) return hipSuccess;
+    if (x->p) (void)hipFree(x->p);
+    x->p = nullptr;
+    x->bytes = 0;
+    const size_t nb = std::max<size_t>(bytes + bytes / 8, 1u << 20);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&x->p), nb);
+    if (e == hipSuccess) x->bytes = nb;
+    return e;
+}
+
+// Peer access from `dev` to `home` (both directions of a part's traffic run
+// on dev's stream: its copy engine reads the home buffer and writes the
+// digests back), enabled once per pair.
+std::mutex g_peer_mu;
+uint8_t g_peer[64][64];   // 0 unknown, 1 enabled, 2 unavailable
+std::atomic<uint64_t> g_st_calls{0}, g_st_remote{0}, g_st_before_wait{0};
+
+void ensure_peer(int dev, int home) {
+    if (dev == home) return;
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    if (g_peer[dev][home]) return;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dev, home) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        g_peer[dev][home] = 2;
+        return;
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    const hipError_t e = hipDeviceEnablePeerAccess(home, 0);
+    (void)hipSetDevice(cur);
+    if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        g_peer[dev][home] = 1;
+    } else {
+        (void)hipGetLastError();
+        g_peer[dev][home] = 2;
+    }
+}
 
 // `ready`: an event on the home device recorded on the caller's stream at
 // entry; every part's stream waits on it before touching the batch, so the
 // parts run after the caller's earlier work on its stream (ABI v4).
+// A remote part (another device, or every part but the first with
+// COPY_PARTS) gets, on its own slot stream and without any host wait: its
+// byte span, its offsets and lengths (peer copies from the home buffers;
+// the data pointer is rebased instead of the offsets: a.data = copy - base),
+// the batch, and the copy of its digests back.  The host waits for the
+// parts only after the last one is enqueued.
 int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, size_t key_len,
                  const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, uint64_t stride,
                  uint32_t fixed_len, uint8_t* digests, const std::vector<uint64_t>& h_off,
                  const std::vector<uint32_t>& h_len, bool copy_all, hipEvent_t ready) {
     const size_t D = dsize(alg);
     const int home = parts[0].dev;
-    std::vector<DevPart> dp(parts.size());
+    std::vector<PartSlot*> slots(parts.size(), nullptr);
     int rc = 0;
     int cur = 0;
     (void)hipGetDevice(&cur);
     auto fail = [&](hipError_t e) { if (!rc && e != hipSuccess) rc = map_err(e); return e != hipSuccess; };
+    uint64_t remote = 0;
+    g_st_calls.fetch_add(1, std::memory_order_relaxed);
     for (size_t k = 0; k < parts.size() && !rc; ++k) {
         const Part& p = parts[k];
         if (p.hi <= p.lo) continue;
         const uint64_t n = p.hi - p.lo;
-        DevPart& q = dp[k];
-        if (fail(hipSetDevice(p.dev)) || fail(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking)) ||
-            fail(hipStreamWaitEvent(q.s, ready, 0)))
-            break;
+        ensure_peer(p.dev, home);
+        if (fail(hipSetDevice(p.dev))) break;
+        PartSlot* q = slot_acquire(p.dev);
+        if (!q) { rc = ENOMEM; break; }
+        slots[k] = q;
+        if (fail(hipStreamWaitEvent(q->s, ready, 0))) break;
         if (p.dev == home && !(copy_all && k > 0)) {  // in place on the home device
             rc = batch_device(alg, key, key_len, offsets ? data : data + p.lo * stride,
                               offsets ? offsets + p.lo : nullptr, lengths ? lengths + p.lo : nullptr, n,
-                              stride, fixed_len, digests + p.lo * D, q.s, nullptr);
+                              stride, fixed_len, digests + p.lo * D, q->s, nullptr);
             continue;
         }
         // Remote part: its byte span [base, end) of the home buffer.
         uint64_t base, end;
-        std::vector<uint64_t> roff;
         if (offsets || lengths) {
             base = UINT64_MAX; end = 0;
             for (uint64_t i = p.lo; i < p.hi; ++i) {
@@ -141,44 +224,40 @@ int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, si
                 base = std::min(base, o);
                 end = std::max(end, o + l);
             }
-            roff.resize(n);
-            for (uint64_t i = p.lo; i < p.hi; ++i) roff[i - p.lo] = (offsets ? h_off[i] : i * stride) - base;
         } else {
             base = p.lo * stride;
             end = (p.hi - 1) * stride + fixed_len;
         }
         const uint64_t span = end > base ? end - base : 0;
-        if (fail(hipMalloc(reinterpret_cast<void**>(&q.data), std::max<uint64_t>(span, 1))) ||
-            fail(hipMalloc(reinterpret_cast<void**>(&q.dig), n * D)))
-            break;
-        if (span && fail(hipMemcpyPeerAsync(q.data, p.dev, data + base, home, span, q.s))) break;
-        if (offsets || lengths) {
-            if (fail(hipMalloc(reinterpret_cast<void**>(&q.off), n * 8)) ||
-                fail(hipMalloc(reinterpret_cast<void**>(&q.len), n * 4)) ||
-                fail(hipMemcpyAsync(q.off, roff.data(), n * 8, hipMemcpyHostToDevice, q.s)))
-                break;
-            std::vector<uint32_t> rl(n);
-            for (uint64_t i = 0; i < n; ++i) rl[i] = lengths ? h_len[p.lo + i] : fixed_len;
-            if (fail(hipMemcpyAsync(q.len, rl.data(), n * 4, hipMemcpyHostToDevice, q.s)) ||
-                fail(hipStreamSynchronize(q.s)))  // roff / rl are stack temporaries
-                break;
-            rc = batch_device(alg, key, key_len, q.data, q.off, q.len, n, 0, 0, q.dig, q.s, nullptr);
+        // Slot buffer: [data span | offsets | lengths | digests], 256-B aligned pieces.
+        auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+        const uint64_t o_data = 0, o_off = up(std::max<uint64_t>(span, 1));
+        const uint64_t o_len = o_off + (offsets ? up(n * 8) : 0);
+        const uint64_t o_dig = o_len + (lengths ? up(n * 4) : 0);
+        if (fail(slot_reserve(q, o_dig + up(n * D)))) break;
+        uint8_t* qd = q->p + o_data;
+        uint64_t* qo = offsets ? reinterpret_cast<uint64_t*>(q->p + o_off) : nullptr;
+        uint32_t* ql = lengths ? reinterpret_cast<uint32_t*>(q->p + o_len) : nullptr;
+        uint8_t* qg = q->p + o_dig;
+        if (span && fail(hipMemcpyPeerAsync(qd, p.dev, data + base, home, span, q->s))) break;
+        if (qo && fail(hipMemcpyPeerAsync(qo, p.dev, offsets + p.lo, home, n * 8, q->s))) break;
+        if (ql && fail(hipMemcpyPeerAsync(ql, p.dev, lengths + p.lo, home, n * 4, q->s))) break;
+        if (offsets) {
+            // message i at (qd - base) + offsets[i]: the copy of the span.
+            rc = batch_device(alg, key, key_len, qd - base, qo, ql, n, 0, fixed_len, qg, q->s, nullptr);
         } else {
-            rc = batch_device(alg, key, key_len, q.data, nullptr, nullptr, n, stride, fixed_len, q.dig, q.s,
-                              nullptr);
+            rc = batch_device(alg, key, key_len, qd, nullptr, ql, n, stride, fixed_len, qg, q->s, nullptr);
         }
-        if (!rc) fail(hipMemcpyPeerAsync(digests + p.lo * D, home, q.dig, p.dev, n * D, q.s));
+        if (!rc && !fail(hipMemcpyPeerAsync(digests + p.lo * D, home, qg, p.dev, n * D, q->s))) ++remote;
     }
+    g_st_remote.fetch_add(remote, std::memory_order_relaxed);
+    if (!rc) g_st_before_wait.fetch_add(remote, std::memory_order_relaxed);
     for (size_t k = 0; k < parts.size(); ++k) {
-        DevPart& q = dp[k];
-        if (!q.s) continue;
-        (void)hipSetDevice(parts[k].dev);
-        fail(hipStreamSynchronize(q.s));
-        if (q.data) (void)hipFree(q.data);
-        if (q.off) (void)hipFree(q.off);
-        if (q.len) (void)hipFree(q.len);
-        if (q.dig) (void)hipFree(q.dig);
-        (void)hipStreamDestroy(q.s);
+        PartSlot* q = slots[k];
+        if (!q) continue;
+        (void)hipSetDevice(q->dev);
+        fail(hipStreamSynchronize(q->s));
+        slot_release(q);
     }
     (void)hipSetDevice(cur);
     return rc;
@@ -253,6 +332,21 @@ int lcb_hash_batch_multi(const int* devs, int ndev, int alg, const uint8_t* key,
         return rc;
     }
     return multi_host(parts, alg, key, key_len, data, offsets, lengths, stride, fixed_len, digests);
+}
+
+int lcb_hash_multi_stats(lcb_hash_multi_stats_t* out) {
+    if (!out) return EINVAL;
+    memset(out, 0, sizeof(*out));
+    out->calls = g_st_calls.load();
+    out->remote_parts = g_st_remote.load();
+    out->parts_enqueued_before_wait = g_st_before_wait.load();
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    for (int a = 0; a < 64; ++a)
+        for (int b = 0; b < 64; ++b) {
+            out->peer_enabled += g_peer[a][b] == 1;
+            out->peer_unavailable += g_peer[a][b] == 2;
+        }
+    return 0;
 }
 
 }  // extern "C"

@@ -27,7 +27,7 @@ __all__ = [
     "sha1_get_digest_batch", "sha1_hmac_get_digest_batch", "sha2_get_digest_batch",
     "sha2_hmac_get_digest_batch", "gost3411_2012_get_digest_batch",
     "gost3411_2012_hmac_get_digest_batch", "gen_synthetic", "sha2_alg", "gost_alg",
-    "partition", "hash_batch_multi", "hash_batch_keyed", "KEY_HMAC", "KEY_PREFIX", "KEY_SUFFIX",
+    "partition", "hash_batch_multi", "multi_stats", "hash_batch_keyed", "KEY_HMAC", "KEY_PREFIX", "KEY_SUFFIX",
 ]
 
 
@@ -296,6 +296,16 @@ def hash_batch_multi(devs, alg, data, *, offsets=None, lengths=None, count=None,
                                      lengths.ctypes.data if lengths is not None else None,
                                      count, stride, fixed_len, out.ctypes.data, 0, None))
     return out
+
+
+def multi_stats():
+    """lcb_hash_multi_stats as a dict: device-mode lcb_hash_batch_multi calls,
+    remote parts, remote parts fully enqueued before the call's first wait,
+    device pairs with peer access enabled / unavailable."""
+    from ._lib import MultiStats
+    st = MultiStats()
+    check(lib().lcb_hash_multi_stats(ctypes.byref(st)))
+    return {n: int(getattr(st, n)) for n, _ in MultiStats._fields_}
 
 
 def hash_batch_keyed(alg, mode, keys, data, *, key_index=None, offsets=None, lengths=None, count=None,

@@ -146,3 +146,32 @@ def test_multi_c5_eight_parts_copy(gpu):
     assert hashlib.sha256(got.cpu().numpy().tobytes()).hexdigest() == fx["algs"]["md5"]["dod"]
     del data, got
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_multi_ragged_c4_shape_copies_before_wait(gpu):
+    """VERDICT r4 item 2: a C4-shaped ragged batch ({64 B, 1 KiB, 64 KiB}
+    lengths, packed) over 8 parts on device 0 with the peer-copy path forced:
+    every remote part's copies, batch and digest copy-back are enqueued
+    before the call waits for any part (lcb_hash_multi_stats), the parts run
+    from pooled slots (repeat calls), and the digests equal the single-device
+    batch."""
+    import torch
+    from tests.golden_util import mixed_lengths
+    n = 24000
+    lens = np.array(mixed_lengths(0x51, n), dtype=np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    data = gpu.gen_synthetic(0x51, int(lens.sum()) + 64)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda:0")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda:0")
+    for alg in (1, 6):
+        ref = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        for rep in range(2):
+            before = gpu.multi_stats()
+            got = gpu.hash_batch_multi([0] * 8, alg, data, offsets=do, lengths=dl, copy_parts=True)
+            after = gpu.multi_stats()
+            assert np.array_equal(got.cpu().numpy(), ref), (alg, rep)
+            assert after["calls"] - before["calls"] == 1
+            assert after["remote_parts"] - before["remote_parts"] == 7
+            assert after["parts_enqueued_before_wait"] - before["parts_enqueued_before_wait"] == 7
