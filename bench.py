@@ -697,6 +697,14 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
         zc_half = run(["--zerocopy", "1", "--rate", str(int(zc["packets_per_s"] / 2))])
     except RuntimeError as e:
         return {"error": str(e)}
+    def stages(r):
+        # The queue's per-stage maxima of the run (lcb_hash_queue_stats), so
+        # each run attributes its own latency tail: first
+        # packet -> seal, seal -> enqueued, GPU, callbacks, longest blocked
+        # submit; where the worst packet sat in the run; blocked submits.
+        return {k: r.get(k) for k in ("max_fill_us", "max_launch_us", "max_gpu_us", "max_callback_us",
+                                      "max_submit_wait_us", "submit_waits", "worst_at", "lat_us_max",
+                                      "late_half_p99")}
     return {"packets_per_s": sat["packets_per_s"], "GiB_s": sat["GiB_s"], "batches": sat["batches"],
             # Zero-copy submit (LCB_HASH_Q_F_ZEROCOPY): packets already in a
             # registered page-locked pool (the io_buf receive buffers,
@@ -705,7 +713,9 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
             "zerocopy": {"packets_per_s": zc["packets_per_s"], "GiB_s": zc["GiB_s"], "batches": zc["batches"],
                          "saturated_lat_us_p50": zc["lat_us_p50"], "saturated_lat_us_p99": zc["lat_us_p99"],
                          "half_load_lat_us_p50": zc_half["lat_us_p50"], "half_load_lat_us_p99": zc_half["lat_us_p99"],
+                         "saturated_stages": stages(zc), "half_load_stages": stages(zc_half),
                          "path": "registered page-locked packet -> H2D in place -> kernel -> D2H -> callback"},
+            "saturated_stages": stages(sat), "half_load_stages": stages(half),
             "saturated_lat_us_p50": sat["lat_us_p50"], "saturated_lat_us_p99": sat["lat_us_p99"],
             "half_load_packets_per_s": half["packets_per_s"], "half_load_lat_us_p50": half["lat_us_p50"],
             "half_load_lat_us_p99": half["lat_us_p99"], "half_load_lat_us_p999": half["lat_us_p999"],

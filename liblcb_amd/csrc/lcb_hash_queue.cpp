@@ -25,6 +25,8 @@
 // completion mirrors tpt_msg_send() (src/threadpool/threadpool_msg_sys.c:279).
 #include <errno.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -104,7 +106,6 @@ struct Slot {
     uint8_t* d_data = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
-    uint8_t* d_dig = nullptr;
     uint32_t* d_work = nullptr;                  // bucketing scratch (launch_ordered)
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -333,20 +334,39 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
     hipStream_t st = b->stream;
     KArgs a;
     a.data = nullptr; a.offsets = b->d_off; a.lengths = b->d_len; a.order = nullptr;
-    a.count = b->n; a.stride = 0; a.fixed_len = 0; a.digests = b->d_dig; a.mid = mid;
+    // The batch kernel stores the digests straight into the slot's pinned,
+    // coherent host buffer: no device -> host copy command per batch.  (The
+    // copy's enqueue blocked the flusher for 8-10 ms once per zero-copy run
+    // -- the p99 half-load tail of BENCH_r04 -- LCB_QUEUE_TRACE)
+    a.count = b->n; a.stride = 0; a.fixed_len = 0; a.digests = b->h_dig; a.mid = mid;
     int rc = 0;
+    // LCB_QUEUE_TRACE=1: report any launch step over 1 ms on stderr
+    // (diagnostics of the zero-copy latency tail).
+    static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+    int64_t tt[8];
+    int nt = 0;
+    tt[nt++] = now_ns();
     if (hipMemcpyAsync(b->d_off, b->h_off, b->n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b->d_len, b->h_len, b->n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
         (aused && hipMemcpyAsync(b->d_data, b->h_data, aused, hipMemcpyHostToDevice, st) != hipSuccess))
         rc = EIO;
+    tt[nt++] = now_ns();
     for (int k = 0; k < nrun && !rc; ++k)
         if (rhost[k] && run[k].hi > run[k].lo &&
             hipMemcpyAsync(b->d_data + rpos[k], rhost[k], run[k].hi - run[k].lo, hipMemcpyHostToDevice, st) != hipSuccess)
             rc = EIO;
+    tt[nt++] = now_ns();
     if (!rc) rc = launch_ordered(alg, a, st, b->d_work);
-    if (!rc && hipMemcpyAsync(b->h_dig, b->d_dig, b->n * D, hipMemcpyDeviceToHost, st) != hipSuccess)
-        rc = EIO;
+    tt[nt++] = now_ns();
+    tt[nt++] = now_ns();
     if (!rc && hipEventRecord(b->done, st) != hipSuccess) rc = EIO;
+    tt[nt++] = now_ns();
+    if (trace && tt[nt - 1] - tt[0] > 1000000)
+        fprintf(stderr, "lcb_hash_queue: slow launch seq=%llu n=%zu runs=%d aused=%llu: idx/len %.0f us, runs %.0f us, "
+                "kernel %.0f us, -- %.0f us, event %.0f us\n", (unsigned long long)b->seq, b->n, nrun,
+                (unsigned long long)aused,
+                (tt[1] - tt[0]) * 1e-3, (tt[2] - tt[1]) * 1e-3, (tt[3] - tt[2]) * 1e-3, (tt[4] - tt[3]) * 1e-3,
+                (tt[5] - tt[4]) * 1e-3);
     b->launch_err = rc;
     b->t_launch = now_ns();
     batches.fetch_add(1, std::memory_order_relaxed);
@@ -419,6 +439,10 @@ void lcb_hash_queue_s::flusher_main() {
         const int64_t t_busy = now_ns();
         drain_leases(b);
         const int64_t t_launch = now_ns();
+        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+        if (trace && (t_launch - t_busy > 1000000 || t_busy - b->t_seal > 1000000))
+            fprintf(stderr, "lcb_hash_queue: slow seal -> launch: reopen %.0f us, drain %.0f us\n",
+                    (t_busy - b->t_seal) * 1e-3, (t_launch - t_busy) * 1e-3);
         const int64_t t_seal = b->t_seal;
         launch(b, why);   // b may complete and be reused from here on: no access
         const int64_t t_end = now_ns();
@@ -499,11 +523,11 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     Q_TRY(hipHostMalloc(reinterpret_cast<void**>(&b.h_data), bytes, hipHostMallocDefault));
     Q_TRY(hipHostMalloc(reinterpret_cast<void**>(&b.h_off), msgs * 8, hipHostMallocDefault));
     Q_TRY(hipHostMalloc(reinterpret_cast<void**>(&b.h_len), msgs * 4, hipHostMallocDefault));
-    Q_TRY(hipHostMalloc(reinterpret_cast<void**>(&b.h_dig), msgs * D, hipHostMallocDefault));
+    // Fine-grained (coherent): the batch kernels write it over the link.
+    Q_TRY(hipHostMalloc(reinterpret_cast<void**>(&b.h_dig), msgs * D, hipHostMallocCoherent));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_data), bytes));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_off), msgs * 8));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_len), msgs * 4));
-    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_dig), msgs * D));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), bucket_words(msgs) * sizeof(uint32_t)));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
@@ -521,9 +545,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     if (hipMemcpyAsync(b.d_data, b.h_data, bytes, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemcpyAsync(b.d_off, b.h_off, msgs * 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemcpyAsync(b.d_len, b.h_len, msgs * 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
-        hipMemsetAsync(b.d_dig, 0, msgs * D, b.stream) != hipSuccess ||
         hipMemsetAsync(b.d_work, 0, bucket_words(msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
-        hipMemcpyAsync(b.h_dig, b.d_dig, msgs * D, hipMemcpyDeviceToHost, b.stream) != hipSuccess ||
         hipStreamSynchronize(b.stream) != hipSuccess)
         return EIO;
     return 0;
@@ -537,7 +559,6 @@ void free_slot(Slot& b) {
     if (b.d_data) (void)hipFree(b.d_data);
     if (b.d_off) (void)hipFree(b.d_off);
     if (b.d_len) (void)hipFree(b.d_len);
-    if (b.d_dig) (void)hipFree(b.d_dig);
     if (b.d_work) (void)hipFree(b.d_work);
     if (b.done) (void)hipEventDestroy(b.done);
     if (b.stream) (void)hipStreamDestroy(b.stream);
@@ -545,7 +566,7 @@ void free_slot(Slot& b) {
     delete[] b.zrun;
     delete[] b.leases;
     b.h_data = nullptr; b.h_off = nullptr; b.h_len = nullptr; b.h_dig = nullptr; b.meta = nullptr; b.zrun = nullptr;
-    b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_dig = nullptr; b.d_work = nullptr;
+    b.d_data = nullptr; b.d_off = nullptr; b.d_len = nullptr; b.d_work = nullptr;
     b.done = nullptr; b.stream = nullptr; b.leases = nullptr; b.nleases = 0;
 }
 
@@ -624,6 +645,21 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
             if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = EIO;
             q->mid = keep;
         }
+    }
+    if (!rc) {
+        // One empty message through the batch path: the process's first
+        // kernel launch loads the library's code object (4-5 ms, LCB_QUEUE_TRACE),
+        // which would otherwise land on the first batch's packets.
+        Slot& b = q->slots[0];
+        KArgs a;
+        a.data = nullptr; a.offsets = b.d_off; a.lengths = b.d_len; a.order = nullptr;
+        a.count = 1; a.stride = 0; a.fixed_len = 0; a.digests = b.h_dig; a.mid = q->mid;
+        *reinterpret_cast<uint64_t*>(b.h_off) = (uint64_t)reinterpret_cast<uintptr_t>(b.d_data);
+        b.h_len[0] = 0;
+        if (hipMemcpyAsync(b.d_off, b.h_off, 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+            hipMemcpyAsync(b.d_len, b.h_len, 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+            launch_ordered(alg, a, b.stream, b.d_work) != 0 || hipStreamSynchronize(b.stream) != hipSuccess)
+            rc = EIO;
     }
     if (rc) {
         q->release_all();
