@@ -262,6 +262,33 @@ def pmc_clock_ghz(alg):
         return None
 
 
+LDS_BYTES_PER_CLK_CU = 256   # ds_read_b64 array rate per CU (MI355X_MICROARCH.md LDS)
+N_CUS = 256
+
+
+def gost_lds_array(name, count, kernel_ms):
+    """GOST against the LDS array's peak: the table
+    gathers' bytes -- 1 KiB message = 17 g_N + 2 g_0 = 19 g x 25 LPS, each 64
+    ds_read_b64 of 8 B: 475 x 512 B -- over the kernel time, as a fraction of
+    256 B/clk/CU x 256 CUs at 2.4 GHz and at the PMC-measured clock, plus the
+    bank-conflict share of the LDS-array cycles from the committed counters
+    (profiles/pmc_gost_lds.json, when its code stamp matches)."""
+    lps = (MSG_LEN // 64 + 1 + 2) * 25
+    gbytes = count * lps * 64 * 8
+    out = {"lds_gather_bytes": gbytes,
+           "lds_array_frac": round(gbytes / (kernel_ms * 1e-3) / (LDS_BYTES_PER_CLK_CU * N_CUS * VALU_CLOCK_HZ), 4)}
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_gost_lds.json")))["kernels"][name]
+        if counters_current(rec):
+            out["lds_bank_conflict_share"] = rec["bank_conflict_share"]
+    except (OSError, ValueError, KeyError):
+        pass
+    clk = pmc_clock_ghz(ALG_IDS[name])
+    if clk:
+        out["lds_array_frac_pmc_clock"] = round(gbytes / (kernel_ms * 1e-3) / (LDS_BYTES_PER_CLK_CU * N_CUS * clk * 1e9), 4)
+    return out
+
+
 def read_probes(data, count, steps=50, warmup=20):
     """Achievable HBM read rate on this box, GB/s: the digest
     kernels' own LDS-DMA line stream over the same records without the
@@ -865,6 +892,12 @@ def main():
                          "kernel_ms": round(km, 4),
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "valu_frac": round(vf / km, 4) if vf else None}
+            clk = pmc_clock_ghz(aid)
+            if vf and clk:
+                # The same floor at the clock the PMC pass measured under this
+                # kernel (the power manager's, not the spec 2.4 GHz).
+                per[name]["pmc_clock_GHz"] = clk
+                per[name]["valu_frac_pmc_clock"] = round(vf * (VALU_CLOCK_HZ / 1e9 / clk) / km, 4)
             if name.startswith("gost"):
                 # GOST is bound by its LDS table gathers, not HBM or VALU:
                 # the gathers alone, same grid and image, beside the kernel.
@@ -874,6 +907,7 @@ def main():
                     lps_ms = per["gost256"]["lps_chain_ms"]
                 per[name]["lps_chain_ms"] = round(lps_ms, 4)
                 per[name]["lds_frac"] = round(lps_ms / km, 4)
+                per[name].update(gost_lds_array(name, count, km))
             del dg
         out["per_alg"] = per
         # Batched HMAC (RADIUS needs HMAC-MD5): per call

@@ -41,7 +41,7 @@ template <int V, int kAux>
 __global__ __launch_bounds__(256) void crc_fixed_lds_kernel(KArgs a) {
     using Var = CrcVar<V>;
     __shared__ uint32_t T[8 * 256];
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][kSlabBytes];
     crc_stage_tables(T, Var::kFam);  // before any early return: it synchronises
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

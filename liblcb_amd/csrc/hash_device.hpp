@@ -697,16 +697,23 @@ __device__ __forceinline__ void load_block_tail(const uint8_t* p, uint32_t rem, 
 // Per-wave LDS-DMA line stream over 64 fixed-stride records (the fixed-stride
 // fast paths of lcb_kernels.hip and crc_kernels.hip).  The per-lane loads of
 // the generic kernels touch 64 different 128-B lines per wave-instruction;
-// here line L of the wave's 64 records moves into an 8 KiB LDS slab with 8
+// here line L of the wave's 64 records moves into a slab of LDS with 8
 // coalesced LDS-DMA instructions (global_load_lds_dwordx4: one instruction =
 // 8 records x one whole 128-B line), every lane copies its own 128 B into
 // VGPRs (take), and the caller issues line L+1 before computing line L.
-// 16-B chunks are XOR-swizzled (chunk k of local record j sits in slot
-// k ^ ((j >> 1) & 7)) so the 16-lane ds_read_b128 groups are conflict-free.
+// Instruction g carries records j with j & 7 == g (lane group q = j >> 3,
+// chunk c = lane & 7) and lands at slab + g * kSlabRow, kSlabRow = 1,040:
+// record j's row starts at (j & 7) * 1040 + (j >> 3) * 128, in bank group
+// ((j & 7) + 8 (j >> 3)) mod 16, so the 16 lanes of every ds_read_b128 group
+// start in 16 different bank groups and take() reads chunk k at row + 16 k,
+// one base and immediate offsets (round 4's 8 KiB slabs XOR-swizzled the
+// chunks: one v_xor per chunk, 8 VALU per line).
 // The fixed-stride stream (LdsStridedStream) always covers 64 whole records;
 // the ragged one (GatherLineStream) repeats a record's last line once it has
 // run out.  The fixed-stride DMA carries the nt cache policy (every byte is
 // read once; kLdsAux).
+constexpr uint32_t kSlabRow = 1040;                     // LDS bytes per DMA instruction (padded)
+constexpr uint32_t kSlabBytes = 7 * kSlabRow + 1024;     // one wave's slab (8,304 B)
 // Default cache policy of the ragged (gather) line stream: a record of a
 // packed ragged batch need not start on a 128-B line, so one streamed "line"
 // can span two cache lines; with nt the second is gone before the record's
@@ -723,23 +730,19 @@ constexpr int kLdsAux = LCB_LDS_AUX;  // cache policy of the LDS-DMA stream: nt 
 struct LdsLineSlab {
     uint8_t* slab;
     uint32_t lane;
-    // Waits for the issued line, copies this lane's 128 B of buffer `buf`
-    // (raw LE words); the buffer is free again on return.
-    __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16], uint32_t buf = 0) const {
+    // Waits for the issued line, copies this lane's 128 B (raw LE words);
+    // the slab is free again on return.
+    __device__ __forceinline__ void take(uint32_t w0[16], uint32_t w1[16]) const {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // LDS byte address of slot (k ^ fj): the row is 128-B aligned, so it
-        // is one v_xor of this lane's base with k << 4.  The base is hidden
-        // from the optimiser each call so the 8 addresses are re-formed here
-        // instead of being hoisted out of the caller's line loop (where they
-        // were spilled to scratch at 80 VGPRs).
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         using lds_cu4 = __attribute__((address_space(3))) const v4u;
-        uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) + buf * 8192 +
-                     lane * 128 + ((lane >> 1) & 7) * 16;
-        asm volatile("" : "+v"(b));
+        // The row base (one VGPR); the 8 chunks at immediate offsets.
+        const uint32_t b = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)slab) +
+                           (lane & 7u) * kSlabRow + (lane >> 3) * 128u;
+        lds_cu4* row = (lds_cu4*)(uintptr_t)b;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const v4u v = *(lds_cu4*)(uintptr_t)(b ^ (uint32_t)(k << 4));
+            const v4u v = row[k];
             uint32_t* d = (k < 4) ? (w0 + 4 * k) : (w1 + 4 * (k - 4));
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
@@ -748,42 +751,39 @@ struct LdsLineSlab {
 };
 
 // Fixed-stride stream with a wave-uniform base: instruction g of line L reads
-// from (wave base + 8 g stride + 128 L) — a scalar address — plus one of two
-// per-lane 32-bit offsets (record lane >> 3 and the chunk, for even and odd
-// g), i.e. the saddr form of global_load_lds with 2 VGPRs of addressing
-// instead of 8 64-bit pointers.  The wave covers 64 whole records (the caller
-// shifts a partial last wave back over its predecessor's records), so there
-// is no per-lane clamp.  Needs 7 * stride + 128 < 2^32.
+// from (wave base + g stride + 128 L) — a scalar address — plus one per-lane
+// 32-bit offset (record 8 (lane >> 3) of the 8 the instruction carries, and
+// the chunk lane & 7), i.e. the saddr form of global_load_lds with 1 VGPR of
+// addressing instead of 8 64-bit pointers.  The wave covers 64 whole records
+// (the caller shifts a partial last wave back over its predecessor's
+// records), so there is no per-lane clamp.  Needs 56 * stride + 128 < 2^32
+// (fixed_stride_lines: stride < 2^26).
 struct LdsStridedStream : LdsLineSlab {
     const uint8_t* wbase;   // wave-uniform
-    uint64_t stride8;       // wave-uniform: 8 records
-    uint32_t voff[2];
+    uint64_t stride1;       // wave-uniform: one record
+    uint32_t voff;
     __device__ __forceinline__ void init(const uint8_t* data, uint64_t stride, uint64_t wave_first, uint32_t ln,
                                          uint8_t* my_slab) {
         lane = ln;
         slab = my_slab;
         wbase = data + wave_first * stride;
-        stride8 = 8 * stride;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const uint32_t f = ((ln >> 4) + 4 * p) & 7;
-            voff[p] = (ln >> 3) * (uint32_t)stride + ((ln & 7) ^ f) * 16;
-        }
+        stride1 = stride;
+        voff = (ln >> 3) * 8u * (uint32_t)stride + (ln & 7) * 16;
     }
     template <int kAux = kLdsAux>
     __device__ __forceinline__ void issue(uint64_t L) {
-        // Offsets re-defined in place (no copy): zero-extended at each use, so
+        // Offset re-defined in place (no copy): zero-extended at each use, so
         // every DMA takes the saddr + 32-bit vaddr form.
-        asm volatile("" : "+v"(voff[0]), "+v"(voff[1]));
+        asm volatile("" : "+v"(voff));
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             // Opaque scalar: keeps the loop optimiser from turning the
             // address into a per-lane 64-bit induction variable.
-            uint64_t so = (uint64_t)g * stride8 + L * 128;
+            uint64_t so = (uint64_t)g * stride1 + L * 128;
             asm volatile("" : "+s"(so));
             const uint8_t* sb = wbase + so;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff[g & 1]),
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(sb + voff),
+                                             (__attribute__((address_space(3))) void*)(slab + g * kSlabRow), 16, 0,
                                              kAux);
         }
     }
@@ -794,7 +794,7 @@ struct LdsStridedStream : LdsLineSlab {
 // (the data is discarded; every DMA stays inside the record).  Bases and
 // limits are exchanged across lanes once, at init.
 struct GatherLineStream : LdsLineSlab {
-    const uint8_t* src[8];  // instruction g: this lane's chunk of local record 8g + (lane >> 3)
+    const uint8_t* src[8];  // instruction g: this lane's chunk of local record g + 8 (lane >> 3)
     uint32_t rem[8];   // advances left: lines of the record after the current one
     __device__ __forceinline__ void init_gather(const uint8_t* base, uint32_t last_line, uint32_t ln,
                                                 uint8_t* my_slab) {
@@ -802,11 +802,10 @@ struct GatherLineStream : LdsLineSlab {
         slab = my_slab;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const int j = 8 * g + (int)(ln >> 3);
+            const int j = g + 8 * (int)(ln >> 3);
             const uint64_t b = __shfl((unsigned long long)reinterpret_cast<uintptr_t>(base), j, 64);
             rem[g] = (uint32_t)__shfl((int)last_line, j, 64);
-            const uint32_t f = ((ln >> 4) + 4 * g) & 7;
-            src[g] = reinterpret_cast<const uint8_t*>(b) + ((ln & 7) ^ f) * 16;
+            src[g] = reinterpret_cast<const uint8_t*>(b) + (ln & 7) * 16;
         }
     }
     // Issues the next line of every record, then steps each record's pointer
@@ -821,7 +820,7 @@ struct GatherLineStream : LdsLineSlab {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[g],
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             (__attribute__((address_space(3))) void*)(slab + g * kSlabRow), 16, 0,
                                              kAux);
             src[g] += 128;
         }
@@ -830,7 +829,7 @@ struct GatherLineStream : LdsLineSlab {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[g],
-                                             (__attribute__((address_space(3))) void*)(slab + g * 1024), 16, 0,
+                                             (__attribute__((address_space(3))) void*)(slab + g * kSlabRow), 16, 0,
                                              kGatherAux);
             const bool more = rem[g] != 0;
             src[g] += more ? 128 : 0;
@@ -887,7 +886,10 @@ __device__ __forceinline__ void wave_prio_left(uint64_t left) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
-template <class H, bool kPf = false>
+// kPrio: the per-lane loop sets the wave priority by the bytes left
+// (LCB_LANE_PRIO); off where the caller keeps its own priority (the resident
+// grid's chunks-left priority in md_fixed_finish).
+template <class H, bool kPf = false, bool kPrio = true>
 __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p, uint64_t nfull) {
     uint32_t w[H::kWords];
     uint64_t b = 0;
@@ -917,7 +919,7 @@ __device__ __forceinline__ const uint8_t* md_full_blocks(H& st, const uint8_t* p
     }
     for (; b < nfull; ++b, p += H::kBlock) {
 #if LCB_LANE_PRIO
-        if ((b & 15) == 0) wave_prio_left((nfull - b) * (uint64_t)H::kBlock);
+        if (kPrio && (b & 15) == 0) wave_prio_left((nfull - b) * (uint64_t)H::kBlock);
 #endif
         load_block_full<H>(p, w);
         st.compress(w);
@@ -943,11 +945,11 @@ __device__ __forceinline__ void md_pad_tail(H& st, uint32_t* w, uint32_t rem, ui
     st.compress(w);
 }
 
-template <class H, bool kPf = false>
+template <class H, bool kPf = false, bool kPrio = true>
 __device__ __forceinline__ void md_message(H& st, const uint8_t* msg, uint64_t len, uint64_t prefix) {
     uint32_t w[H::kWords];
     const uint64_t nfull = len / H::kBlock;
-    const uint8_t* p = md_full_blocks<H, kPf>(st, msg, nfull);
+    const uint8_t* p = md_full_blocks<H, kPf, kPrio>(st, msg, nfull);
     const uint32_t rem = (uint32_t)(len - nfull * H::kBlock);
     load_block_tail<H>(p, rem, w);
     md_pad_tail(st, w, rem, len + prefix);

@@ -51,13 +51,13 @@ __device__ __forceinline__ bool batch_aborted(const KArgs& a) {
 enum { kKeyNone = 0, kKeyHmac = 1, kKeyPrefix = 2, kKeySuffix = 3 };
 
 // Fixed-stride batch of at least 64 16-B aligned records with at least one
-// whole 128-B line each and a stride below 256 MiB: the shape the LDS-DMA
-// line-stream kernels accept (LdsStridedStream: whole 64-record waves,
-// 32-bit per-lane offsets).
+// whole 128-B line each and a stride below 64 MiB: the shape the LDS-DMA
+// line-stream kernels accept (LdsStridedStream: whole 64-record waves, one
+// 32-bit per-lane offset up to 56 strides).
 inline bool fixed_stride_lines(const KArgs& a) {
     return !a.offsets && !a.lengths && !a.order && (a.stride % 16) == 0 &&
            (reinterpret_cast<uintptr_t>(a.data) % 16) == 0 && a.fixed_len >= 128 && a.stride >= a.fixed_len &&
-           a.count >= 64 && a.stride < (1ull << 28);
+           a.count >= 64 && a.stride < (1ull << 26);
 }
 
 // Words reserved per HMAC mid-state (GOST needs 34: h, N, Sigma).

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t seed, uint64_t start,
 //            measured slower: 5.3 against 5.6 TB/s).
 // One uint32 per record / per thread goes to `sink` so nothing is dead.
 __global__ __launch_bounds__(256) void probe_records_kernel(KArgs a, uint32_t* sink) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][kSlabBytes];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint64_t wave_first = ((uint64_t)blockIdx.x * 4 + wv) * 64;

@@ -157,8 +157,8 @@ __device__ __forceinline__ void md_fixed_finish(H& st, const KArgs& a, const uin
     const uint64_t tail = (uint64_t)fixed_len - nlines * 128;
     if (tail == 0)  // wave-uniform: schedule of the pad block on the SALU
         md_pad_only(st, prefix + nlines * 128);
-    else
-        md_message(st, msg, tail, prefix + nlines * 128);
+    else   // the resident grid's chunks-left priority stays (no per-lane bytes-left priority)
+        md_message<H, false, false>(st, msg, tail, prefix + nlines * 128);
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kHmac) {
@@ -172,7 +172,7 @@ __device__ __forceinline__ void md_fixed_finish(H& st, const KArgs& a, const uin
 
 template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][kSlabBytes];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint8_t* data = a.data;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_persist_kernel(KArg
 
 template <class H, bool kHmac, int kAux>
 __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kFixedWaves][kSlabBytes];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint64_t wave_first = ((uint64_t)(LCB_FIXED_XCD ? xcd_block() : blockIdx.x) * kFixedWaves + wv) * 64;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
 #endif
 template <class H, bool kHmac>
 __global__ __launch_bounds__(256, 4) void md_lines_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][8192];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[4][kSlabBytes];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t first = ((uint64_t)blockIdx.x * 4 + wv) * 64;

@@ -317,11 +317,8 @@ __device__ __forceinline__ uint32_t group8_or(uint32_t v) {
 #ifndef LCB_TILE_SKIP
 #define LCB_TILE_SKIP 1
 #endif
-#ifndef LCB_TILE_ROW
-#define LCB_TILE_ROW 1040
-#endif
-constexpr uint32_t kTileRow = LCB_TILE_ROW;             // LDS bytes per DMA instruction (padded)
-constexpr uint32_t kTileSlab = 7 * kTileRow + 1024;     // one wave's slab
+constexpr uint32_t kTileRow = kSlabRow;     // the padded rows of the shared line slab (hash_device.hpp)
+constexpr uint32_t kTileSlab = kSlabBytes;
 struct TileGatherStream {
     uint8_t* slab;
     uint32_t lane;
@@ -483,7 +480,9 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     const int32_t dl = (int32_t)(d >> 7);
     const int32_t dmin = wave_min_i32(dl), dmax = wave_max_i32(dl);
     const uint64_t lo = b0 + (uint64_t)((int64_t)dmin * 128);
-    if (!__all(near) || ((uint64_t)(uint32_t)(dmax - dmin) + NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
+    // The span in lines, in 64 bits (dmax - dmin of two int32 may exceed int32).
+    const uint64_t span_lines = (uint64_t)((int64_t)dmax - (int64_t)dmin);
+    if (!__all(near) || (span_lines + NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
         if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m_.K, m_.kl, 0);
         else md_message(st, r.p, r.len, m_.prefix);
         tile_finish<H, kMode>(a, st, r);
@@ -527,9 +526,34 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // loop unrolled by two so that which buffer holds the carry is fixed at
     // compile time: line L lands in one buffer while the other's upper half
     // (dwords 16..31 of line L - 1) is the carry, merged in place -- no
-    // per-line copy of the carry (16 v_mov per line before).
+    // per-line copy of the carry (16 v_mov per line before).  MD5 only: the
+    // unrolled loop of SHA-1 / SHA-224/256 (~45 KiB of code per dword phase,
+    // four phases hot at once) ran 2.7-2.9 % slower on packets than the
+    // rolled one despite 1.2 % fewer VALU (instruction cache), and their
+    // carry copy is 0.6 % of a line's VALU (profiles/r5_tile_ab.txt).
+    constexpr bool kTwoBuf = std::is_same<H, Md5>::value;
     uint32_t L = 0;
-    if (LF) {
+    if constexpr (!kTwoBuf) {
+        for (; L < LF; ++L) {
+            uint32_t y[32];
+#if LCB_TILE_PRIO
+            if ((L & 15u) == 0) tile_prio(NL - L);
+#endif
+            ls.take(y);
+            LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
+            if (L + 1 < LE) issue(L + 1);
+            uint32_t w[16];
+            if (L > 0) {   // block 2L - 1 - h: the carry merged with this line's wrapped chunks
+                if (rotated) tile_merge(c, y, kp);
+                tile_shift<kR, kA16>(c, y, sh, w);
+                tile_compress(st, w);
+            }
+            tile_shift<kR, kA16>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
+            if (L > 0 || half() == 0) tile_compress(st, w);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+        }
+    } else if (LF) {
         uint32_t ya[32], yb[32];
         // Line L into y, cr = the other buffer's upper half (the carry).
         auto whole_line = [&](uint32_t Ln, uint32_t* y, uint32_t* cr) {

@@ -536,3 +536,36 @@ def test_tiles_pad_heavy(gpu, oracle, mode):
                                        device="cuda"), offsets=do, lengths=dl).cpu().numpy()
             exp = oracle.batch_keyed(alg, mode, KEYS, data, kidx, offs, lens)
         assert np.array_equal(got, exp), (alg, mode)
+
+
+@pytest.mark.gpu
+def test_bucketing_large_chunks(gpu, oracle):
+    """ragged batches above 4M messages bucket in chunks of
+    4097..8192 messages (two unrolled steps per thread, ~1,000 blocks), a
+    path the other tests never reach.  4.5M short messages of many lengths:
+    the whole batch (chunk 4,395) against its two halves (chunk 4,096) and
+    2,000 sampled digests against the oracle, MD5 (tile form, padded runs)
+    and SHA-512 (unpadded form)."""
+    n = 4_500_000
+    rng = np.random.default_rng(45)
+    lens = rng.integers(0, 180, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3)
+    total = int(offs[-1] + lens[-1]) + 64
+    data = gpu.gen_synthetic(0x4545, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    pick = rng.choice(n, 2000, replace=False)
+    host = None
+    for alg in (1, 6):
+        whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        h = n // 2
+        a = gpu.hash_batch(alg, data, offsets=do[:h], lengths=dl[:h]).cpu().numpy()
+        b = gpu.hash_batch(alg, data, offsets=do[h:], lengths=dl[h:]).cpu().numpy()
+        assert np.array_equal(whole, np.concatenate([a, b])), alg
+        if host is None:
+            host = data.cpu().numpy()
+        exp = oracle.batch(alg, host, offs[pick], lens[pick])
+        assert np.array_equal(whole[pick], exp), alg
+    del data
+    torch.cuda.empty_cache()

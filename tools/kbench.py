@@ -20,6 +20,8 @@ p.add_argument("--reps", type=int, default=50)
 p.add_argument("--count", type=int, default=1 << 20)
 p.add_argument("--len", type=int, default=1024)
 p.add_argument("--warmup", type=int, default=60, help="untimed launches per algorithm (clock ramp)")
+p.add_argument("--gost-probe", action="store_true",
+               help="also run the GOST LPS-chain probe (lcb_hash_gpu_read_probe LCB_PROBE_GOST_LPS)")
 a = p.parse_args()
 
 data = liblcb_amd.gen_synthetic(0x6C62636861736821, a.count * a.len)
@@ -43,3 +45,16 @@ for name in a.alg.split(","):
     gb = a.count * a.len
     print("%-8s median %.4f ms  min %.4f ms  %.1f GB/s (min)" % (name, ts[len(ts) // 2], ts[0],
                                                                gb / ts[0] / 1e6), flush=True)
+
+if a.gost_probe:
+    sink = torch.empty(a.count, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        check(lib().lcb_hash_gpu_read_probe(2, None, a.count, a.len, a.len, sink.data_ptr(), s.cuda_stream))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+    for e0, e1 in ev:
+        e0.record(s)
+        check(lib().lcb_hash_gpu_read_probe(2, None, a.count, a.len, a.len, sink.data_ptr(), s.cuda_stream))
+        e1.record(s)
+    torch.cuda.synchronize()
+    ts = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+    print("gost_lps_probe median %.4f ms  min %.4f ms" % (ts[len(ts) // 2], ts[0]), flush=True)

@@ -139,10 +139,36 @@ def main():
                 v["GRBM_GUI_ACTIVE"] = mean(c["GRBM_GUI_ACTIVE"])
             v.update(stamp(k))
             valu[alg] = v
-    occ = occupancy(src, "kb_occ", BENCH_KERNEL["md5"])
-    if occ and "md5" in valu:
-        valu["md5"]["occupancy"] = occ
-        print("md5 occupancy", occ)
+    # Occupancy / clock pass of the VALU-bound kernels.
+    for alg in ("md5", "sha1", "sha256", "sha512", "gost256"):
+        occ = occupancy(src, "kb_occ", BENCH_KERNEL[alg])
+        if occ and alg in valu:
+            valu[alg]["occupancy"] = occ
+            print(alg, "occupancy", occ)
+    # GOST against the LDS array: LDS-array cycles
+    # (SQ_LDS_IDX_ACTIVE), the extra cycles of bank conflicts
+    # (SQ_LDS_BANK_CONFLICT), LDS instructions, of the plain kernel and of
+    # its bare LPS chain.
+    lds = {}
+    lp = passes(src, "kb_lds")
+    for name, k in (("gost256", BENCH_KERNEL["gost256"]), ("gost512", BENCH_KERNEL["gost512"]),
+                    ("lps_probe", "lcbgpu::gost_lps_probe_kernel")):
+        c = lp.get(k)
+        if not c or not c.get("SQ_LDS_IDX_ACTIVE"):
+            print("missing LDS counters for", name)
+            continue
+        r = {n: mean(v) for n, v in c.items()}
+        r["dispatches"] = len(c["SQ_LDS_IDX_ACTIVE"])
+        r["bank_conflict_share"] = round(r.get("SQ_LDS_BANK_CONFLICT", 0) / r["SQ_LDS_IDX_ACTIVE"], 4)
+        r.update(stamp(k))
+        lds[name] = r
+        print(name, "LDS bank-conflict share", r["bank_conflict_share"])
+    if lds:
+        json.dump({"round": tag, "source": os.path.relpath(src, ROOT), "count": 1 << 20, "msg_len": 1024,
+                   "what": "rocprofv3 --pmc over tools/kbench.py --alg gost256,gost512 --gost-probe: SQ_LDS_IDX_ACTIVE "
+                           "= LDS-array cycles, SQ_LDS_BANK_CONFLICT = their extra cycles from bank conflicts "
+                           "(MI355X_MICROARCH.md LDS), SQ_INSTS_LDS, per dispatch means",
+                   "kernels": lds}, open(os.path.join(prof, "pmc_gost_lds.json"), "w"), indent=1)
     if valu:
         json.dump({"what": "SQ_INSTS_VALU (wave-instructions) per launch of each algorithm's kernel on the bench "
                            "workload (1M x 1 KiB, fixed stride), rocprofv3 --pmc, mean over dispatches",

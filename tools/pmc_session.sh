@@ -21,8 +21,12 @@ done
 # MD5 fixed-stride kernel only: wave occupancy and clock (SQ_WAVE_CYCLES /
 # SQ_BUSY_CYCLES), and why the dispatcher could not place a workgroup
 # (SPI resource-allocation stalls: LDS full, workgroup limit).
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS -d $O/kb_occ -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5 --reps 5 --warmup 5 > $O/kb_occ.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS -d $O/kb_occ -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5,sha1,sha256,sha512,gost256 --reps 5 --warmup 5 > $O/kb_occ.log 2>&1
 rc=$?; echo "kb occ rc=$rc"; [ $rc -ne 0 ] && exit $rc
+# GOST: LDS-array cycles, bank-conflict cycles, LDS instructions of the
+# plain kernel and of its bare LPS chain (the probe), with the clock.
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_UNALIGNED_STALL SQ_BUSY_CYCLES SQ_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $O/kb_lds -o run --output-format csv -- python3 $R/tools/kbench.py --alg gost256,gost512 --reps 5 --warmup 3 --gost-probe > $O/kb_lds.log 2>&1
+rc=$?; echo "kb lds rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 90 rocprofv3 --pmc SPI_RA_LDS_CU_FULL_CSN SPI_RA_TGLIM_CU_FULL_CSN -d $O/kb_spi -o run --output-format csv -- python3 $R/tools/kbench.py --alg md5 --reps 5 --warmup 5 > $O/kb_spi.log 2>&1
 rc=$?; echo "kb spi rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VALU -d $O/kt_pktocc -o run --output-format csv -- python3 $R/tools/pkt_bench.py --steps 3 --no-layouts --no-c4 > $O/kt_pktocc.log 2>&1
