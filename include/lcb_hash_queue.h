@@ -99,8 +99,10 @@ typedef struct lcb_hash_queue_stats_s {
  * follows the end of a run within 256 B extends it); every run that lies in
  * one registered region and fits the slot's device arena moves to the device
  * with ONE bulk host-to-device copy, and only a packet outside such a run is
- * read by the kernel in place over PCIe.  The bytes must stay unchanged until
- * the packet's completion (digest written / callback called).  One segment
+ * read by the kernel in place over PCIe (GOST reads each message twice, in
+ * its Sigma pass and its compression pass: such a packet crosses PCIe twice).
+ * The bytes must stay unchanged until the packet's completion (digest
+ * written / callback called).  One segment
  * only (lcb_hash_queue_submitv with nsegs == 1); EINVAL if
  * [data, data + size) is not inside one registered region. */
 #define LCB_HASH_Q_F_ZEROCOPY	0x0002u

@@ -450,6 +450,7 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
     if (kc) {
         a.bad = kc->dflag;
         a.bad_epoch = kc->epoch;
+        a.check_host = kc->fused_host;
     }
     uint8_t* temp = nullptr;
     if (key) {
@@ -460,6 +461,8 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
     }
     int rc;
     const size_t words = ordered_words(a);
+    // A fused check needs this batch's bucketing on the keyed call's scratch.
+    if (kc && kc->fused_host && (words == 0 || kc->work_words < words)) return EINVAL;
     if (kc && kc->work_words >= words) {
         rc = launch_ordered(alg, a, s, kc->work);   // the keyed call's stream scratch
     } else if (words) {
@@ -834,10 +837,15 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
         kc.epoch = ss->epoch;
         kc.work = reinterpret_cast<uint32_t*>(stream_scratch_payload(ss));
         kc.work_words = ss->bytes / sizeof(uint32_t);
-        const uint32_t nblk = launch_key_check(key_index, count, (uint32_t)nkeys, reinterpret_cast<uint32_t*>(ss->p),
-                                               ss->hflag, kc.epoch, ss->ctr, s);
-        ss->ctr += nblk;
-        rc = map_err(hipGetLastError());
+        if (words && kc.work_words >= words) {
+            // Bucketed: the count kernel checks the indices (bucket_count_kernel<true>).
+            kc.fused_host = ss->hflag;
+        } else {
+            const uint32_t nblk = launch_key_check(key_index, count, (uint32_t)nkeys,
+                                                   reinterpret_cast<uint32_t*>(ss->p), ss->hflag, kc.epoch, ss->ctr, s);
+            ss->ctr += nblk;
+            rc = map_err(hipGetLastError());
+        }
         if (!rc)
             rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr,
                               &kt, &kc);

@@ -34,6 +34,10 @@ struct KArgs {
     // stored only while *bad != bad_epoch (batch_aborted).
     const uint32_t* bad = nullptr;
     uint32_t bad_epoch = 0;
+    // Set when the check runs inside the bucketing (launch_bucketing): the
+    // count kernel checks the indices and sets *bad, the base kernel writes
+    // the result to this pinned host word (no separate check kernel).
+    uint32_t* check_host = nullptr;
 };
 
 // True when the key-index check of this keyed batch found an index >= nkeys
@@ -239,6 +243,9 @@ struct KeyCheck {
     uint32_t epoch = 0;
     uint32_t* work = nullptr;
     size_t work_words = 0;
+    // Non-null: the batch is bucketed and its count kernel runs the check
+    // (one kernel less per keyed call); the result goes to this host word.
+    uint32_t* fused_host = nullptr;
 };
 int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
                  const uint64_t* offsets, const uint32_t* lengths, size_t count, uint64_t stride,

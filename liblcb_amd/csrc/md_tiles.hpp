@@ -172,7 +172,18 @@ __device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint6
             const uint32_t part = (w[k] & pm) | pb;
             w[k] = e > (uint32_t)k ? w[k] : (e == (uint32_t)k ? part : 0u);
         }
-        if (m.total != len && m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
+        if constexpr (kMode == kTileKeyedSuffix) {
+            // The key K (the message's suffix: virtual bytes len .. total)
+            // ORed in where it falls in this block (per-lane loads of the
+            // small key table, L2-resident), then its 0x80 terminator.
+            if (pos < m.total) {
+                const uint64_t kb = pos > len ? pos : len;       // first block byte taken from K
+                const uint32_t s0 = (uint32_t)(kb - pos);
+                const uint64_t e = pos + 64 < m.total ? pos + 64 : m.total;
+                or_window64(m.K + (kb - len) - s0, s0, (uint32_t)(e - pos), w);
+            }
+            if (m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
+        }
         if (b + 1 == nblk) H::put_length(w, m.total + m.prefix);
     }
     tile_compress(st, w);
@@ -354,9 +365,14 @@ struct TileGatherStream {
                                              kLdsAux);
     }
     // lastc: index of this lane's last stream chunk holding a record byte;
-    // m: its record's rotation; first: its first chunk holding a record
-    // byte in line L (line 0: start >> 4 & 7; later lines 0).
-    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc, uint32_t m, uint32_t first = 0) {
+    // first: its first chunk holding a record byte in line L (line 0 only,
+    // kFirst: start >> 4 & 7; later lines 0).  The chunk k this lane fetches
+    // for instruction g is voff[g]'s chunk field ((voff[g] >> 4) & 7: the
+    // record's row offset is a multiple of 128), so the group's rotations
+    // need no exchange here (r4 rebuilt them with 3 DPP per call and 3 VALU
+    // per instruction).
+    template <bool kFirst>
+    __device__ __forceinline__ void issue_masked(uint32_t L, uint32_t lastc, uint32_t first = 0) {
         // The lane id re-defined per call: the per-lane chunk numbers below
         // are not hoisted out of the tile loop (16 VGPRs held all along).
         uint32_t ln = lane;
@@ -364,13 +380,13 @@ struct TileGatherStream {
         int n = (int)lastc - 8 * (int)L + 1;                    // valid chunks of line L
         n = n < 0 ? 0 : (n > 8 ? 8 : n);
         const uint32_t nv = group8_or((uint32_t)n << (4u * (ln & 7u)));
-        const uint32_t mpk = group_rot(m, ln);
 #if LCB_TILE_SKIP
-        const uint32_t fv = group8_or(first << (4u * (ln & 7u)));   // every lane active (DPP)
+        uint32_t fv = 0;
+        if constexpr (kFirst) fv = group8_or(first << (4u * (ln & 7u)));   // every lane active (DPP)
 #endif
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint32_t k = ((ln & 7u) + ((mpk >> (2 * g)) & 3u)) & 7u;   // chunk of the line
+            const uint32_t k = (voff[g] >> 4) & 7u;                      // chunk of the line
 #if LCB_TILE_SKIP
             // Only the chunks that hold record bytes are fetched: a lane whose
             // chunk lies past its record's last byte (or, in line 0, before
@@ -382,15 +398,14 @@ struct TileGatherStream {
             // 0 from HBM; lanes switched off by EXEC cost the branches and the
             // saddr form: profiles/r4_tile_skip_ab.txt.)  1M packets: HBM
             // reads 1.237 -> 1.15 x the algorithmic bytes.
-            const uint32_t nk = (nv >> (4 * g)) & 15u, fk = (fv >> (4 * g)) & 15u;
-            const uint32_t t = k < fk ? fk : (k < nk ? k : nk - 1u);
+            const uint32_t nk = (nv >> (4 * g)) & 15u;
+            uint32_t t = k < nk ? k : nk - 1u;
+            if constexpr (kFirst) {
+                const uint32_t fk = (fv >> (4 * g)) & 15u;
+                t = k < fk ? fk : t;
+            }
             const uint32_t v = voff[g] + L * 128u + 16u * t - 16u * k;
-#if LCB_TILE_SKIP == 2
-            const bool any = true;
-#else
-            const bool any = nk != 0;    // the record has bytes in line L (uniform in the lane's group)
-#endif
-            if (any)
+            if (nk != 0)   // the record has bytes in line L (uniform in the lane's group)
                 __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(tb + v),
                                                  (__attribute__((address_space(3))) void*)(slab + g * kTileRow), 16, 0,
                                                  kLdsAux);
@@ -453,9 +468,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     const uint32_t sh = p32 & 3u;
     const uint32_t off = p32 & 127u;              // stream offset of the record's first byte
     const uint32_t h = off >> 6, m = (off >> 4) & 3u;
-    // h and m re-derived from the start at each use (one v_bfe), not held in
-    // VGPRs through the line loop.
-    auto rot = [&]() { uint32_t v = p32; asm volatile("" : "+v"(v)); return (v >> 4) & 3u; };
+    // h re-derived from the start at each use (one v_bfe), not held in a
+    // VGPR through the line loop.
     auto half = [&]() { uint32_t v = p32; asm volatile("" : "+v"(v)); return (v >> 6) & 1u; };
     const uint64_t len = r.len;
     H st;
@@ -491,14 +505,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
     TileGatherStream ls;
     ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(dl - dmin) * 128u, m, lane, slab);
-    // Keyed suffix: the stream ends with the whole-block lines, the rest
-    // (under two lines of message, the key) goes through the per-lane loop:
-    // the key's window assembly next to a streamed line needs more VGPRs
-    // than the occupancy leaves.  Its line count needs the whole geometry.
-    if (kMode != kTileKeyedSuffix) {
-        if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
-        else ls.issue_masked(0, lastc, rot(), off >> 4);
-    }
+    if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
+    else ls.issue_masked<true>(0, lastc, off >> 4);
     // The rest of the geometry: lines wholly inside every record (min),
     // blocks of the padded (virtual) message + h (max), lines whose two
     // blocks are whole message blocks (min), whole message blocks (min).
@@ -513,11 +521,10 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // the carry needs no merge (wave-uniform).
     const bool rotated = !__all(m == 0);
     auto issue = [&](uint32_t L) {
-        if (L >= NS) ls.issue_masked(L, lastc, rot());
+        if (L >= NS) ls.issue_masked<false>(L, lastc);
         else ls.issue(L);
     };
-    const uint32_t LE = kMode == kTileKeyedSuffix ? LF : NL;   // lines streamed
-    if (kMode == kTileKeyedSuffix && LE) issue(0);
+    const uint32_t LE = NL;   // lines streamed
     TileKeep kp;      // the merge's keep masks (lane masks, once per tile)
     kp.init(m);
     uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
@@ -597,14 +604,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             for (int k = 0; k < 16; ++k) c[k] = ya[16 + k];
         }
     }
-    if constexpr (kMode == kTileKeyedSuffix) {
-        const uint32_t nd = LF ? 2u * LF - 1u - half() : 0u;       // blocks 0 .. nd - 1 done
-        const uint64_t done = (uint64_t)nd * 64u;
-        md_message2(st, r.p + done, len - done, m_.K, m_.kl, m_.prefix + done);
-        tile_finish<H, kMode>(a, st, r);
-        return;
-    }
-    // The rest, line by line (tile_block: ends of messages, padding, length);
+    // The rest, line by line (tile_block: ends of messages, a keyed suffix,
+    // padding, length);
     // lines past the last streamed one are zeros (those bytes lie past every
     // record's end).
     for (; 2 * L <= NB; ++L) {   // block 2L - 1 - h < nblk for some lane

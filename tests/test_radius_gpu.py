@@ -61,6 +61,25 @@ def test_keyed_vs_oracle_device(gpu, oracle, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 3])
+def test_keyed_tiles_every_key_length(gpu, oracle, mode):
+    """Device mode above the bucketing threshold: the tile kernel of every
+    64-B-block hash, keyed HMAC and secret suffix, with the 7 keys (0..200
+    bytes: a suffix that ends in the message's last block, spans the next
+    ones, or is empty) at every start byte phase and tail length."""
+    import torch
+    data, offs, lens, kidx = _ragged(40 + mode, 9000)
+    dd = torch.as_tensor(data, device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    dk = torch.as_tensor(kidx.astype(np.int32), device="cuda")
+    for alg in (1, 2, 3, 4):
+        got = gpu.hash_batch_keyed(alg, mode, KEYS, dd, key_index=dk, offsets=do, lengths=dl).cpu().numpy()
+        exp = oracle.batch_keyed(alg, mode, KEYS, data, kidx, offs, lens)
+        assert np.array_equal(got, exp), (alg, mode)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_keyed_vs_oracle_host_and_fixed(gpu, oracle, mode):
     data, offs, lens, kidx = _ragged(20 + mode, 6000)   # above the bucketing threshold
