@@ -741,7 +741,7 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
                          "saturated_lat_us_p50": zc["lat_us_p50"], "saturated_lat_us_p99": zc["lat_us_p99"],
                          "half_load_lat_us_p50": zc_half["lat_us_p50"], "half_load_lat_us_p99": zc_half["lat_us_p99"],
                          "saturated_stages": stages(zc), "half_load_stages": stages(zc_half),
-                         "path": "registered page-locked packet -> H2D in place -> kernel -> D2H -> callback"},
+                         "path": "registered page-locked packet -> bulk H2D run copy (or read in place) -> kernel writes digests to pinned memory -> callback"},
             "saturated_stages": stages(sat), "half_load_stages": stages(half),
             "saturated_lat_us_p50": sat["lat_us_p50"], "saturated_lat_us_p99": sat["lat_us_p99"],
             "half_load_packets_per_s": half["packets_per_s"], "half_load_lat_us_p50": half["lat_us_p50"],

@@ -585,7 +585,7 @@ struct Sha512 {
     template <int i>
     __device__ __forceinline__ static void uround(UVars& v) {
         uint64_t x;
-        if (i < 16) {
+        if constexpr (i < 16) {
             x = v.w[i];
         } else {
             const uint64_t w15 = v.w[(i - 15) & 15], w2 = v.w[(i - 2) & 15];

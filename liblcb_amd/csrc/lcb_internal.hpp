@@ -38,6 +38,9 @@ struct KArgs {
     // count kernel checks the indices and sets *bad, the base kernel writes
     // the result to this pinned host word (no separate check kernel).
     uint32_t* check_host = nullptr;
+    // Segmented long tiles (md_tiles.hpp): per-tile flags, then the saved
+    // states (bucket_seg_words); nullptr: no tile is segmented.
+    uint32_t* seg = nullptr;
 };
 
 // True when the key-index check of this keyed batch found an index >= nkeys
@@ -112,9 +115,35 @@ constexpr uint64_t kBucketMaxCount = 0xffffffffull - 63ull * kBucketKeys;
 inline size_t bucket_order_words(uint64_t count) { return (size_t)count + 64ull * (kBucketKeys + 1); }
 // uint32 words of bucketing scratch for a batch of `count` messages:
 // [work | permutation | per-block counts | per-block bases | 16-bit keys].
-inline size_t bucket_words(uint64_t count) {
-    return (size_t)kBucketWork + bucket_order_words(count) + 2 * bucket_blocks(count) * kBucketKeys + (count + 1) / 2;
+// Segmented long tiles (md_tiles.hpp): when a large batch's longest keys
+// (records of at least kSegMinClass's length, 32 KiB) fill at least one
+// generation of the tile kernel's wave slots, each of their tiles runs as
+// kSegs jobs of a third of its lines, the state handed on through memory.
+// The tile count of a batch is then kSegs x (long tiles) + the rest, fine
+// enough to spread over the SIMDs: a long class of 5,461 tiles is 5.33
+// tiles per SIMD, 6 when whole, 16 thirds when cut.
+constexpr int kSegs = 3;
+constexpr uint32_t kSegMinClass = 67;            // len_class: >= 512 blocks
+constexpr uint32_t kSegStateWords = 16;          // hash state words saved per lane (SHA-512: 8 x 64 bits)
+constexpr uint32_t kLinesOcc = 4;                // md_lines_kernel (SHA-384/512 ragged): waves per SIMD
+constexpr uint32_t kSegHead = 64;                // a.seg[0] = segmented waves; flags from a.seg[kSegHead]
+constexpr uint64_t kSegMinCount = 131072;        // 2 x 4 x 256 SIMD slots of 64 records
+__host__ __device__ inline uint64_t bucket_tiles_max(uint64_t count) { return (count + 63) / 64 + kBucketKeys; }
+// [count | pad to kSegHead | one flag per wave, padded to 64 | kSegStateWords
+// x 64 words per wave].
+__host__ __device__ inline uint64_t bucket_seg_state_offset(uint64_t count) {
+    return kSegHead + (bucket_tiles_max(count) + 63) / 64 * 64;
 }
+inline size_t bucket_seg_words(uint64_t count) {
+    if (count < kSegMinCount) return 0;
+    return (size_t)(bucket_seg_state_offset(count) + bucket_tiles_max(count) * 64 * kSegStateWords);
+}
+inline size_t bucket_seg_offset(uint64_t count) {
+    const size_t w = (size_t)kBucketWork + bucket_order_words(count) + 2 * bucket_blocks(count) * kBucketKeys +
+                     (count + 1) / 2;
+    return (w + 63) / 64 * 64;
+}
+inline size_t bucket_words(uint64_t count) { return bucket_seg_offset(count) + bucket_seg_words(count); }
 
 // CRC-32 variants travel through the batch machinery as alg ids
 // kCrcAlgBase + variant (variant ids of include/lcb_crc32_gpu.h).
@@ -171,7 +200,12 @@ void crc_table_host(int variant, uint32_t* out);
 // lengths/count) into `order` (bucket_order_words(count) words); `work` =
 // kBucketWork words (key totals, entry count).  tiles: the tile kernel's
 // form, each key's run padded to whole tiles when the batch is large.
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, hipStream_t s);
+// seg_min > 0 (a.seg set): segment the waves of the longest keys when there
+// are at least 1.25 x seg_min (wave slots) of them and cutting them evens
+// the SIMDs' load (a.seg[0] = their count, else 0; their flags zeroed).
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, hipStream_t s);
+// The tile kernel's wave slots of alg on this device (0: no tile kernel).
+uint32_t tile_slots(int alg);
 // True when launch_batch(alg, a) runs the tile kernel on a bucketed batch:
 // only then may `order` hold pad entries (every other kernel reads it per lane).
 bool tiles_take(int alg, const KArgs& a);

@@ -250,7 +250,8 @@ template <bool kTiles>
 __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t chunk, uint32_t nb,
                                                             const uint32_t* cnt, const uint32_t* base,
                                                             const uint32_t* tot, const uint16_t* keys,
-                                                            uint32_t* work, uint32_t* order) {
+                                                            uint32_t* work, uint32_t* order, uint32_t seg_min,
+                                                            uint32_t seg_simds, uint32_t* seg_flags) {
     __shared__ uint32_t h[kBucketKeys];        // run start in `order` of this block's entries, per key
     __shared__ uint32_t loc[kBucketKeys];      // local (sorted) offset per key, then the fill cursor
     __shared__ uint32_t len_s[kBucketKeys];
@@ -316,15 +317,43 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
         }
     }
     __syncthreads();
+    constexpr uint32_t kSegKey = kSegMinClass * kBucketPhases;
+    static_assert(kSegKey >= 1 && kSegKey < (uint32_t)kBucketKeys, "segment class inside the key range");
     if (t < (uint32_t)kBucketKeys) {
         const uint32_t start = h[t];
         if (blockIdx.x == 0)
             for (uint32_t e = start + hk; e < start + len_s[t]; ++e) gptr(order)[e] = kOrderPad;
+        // Segmented waves: the runs of every key >= kSegKey (the longest
+        // classes) come first, so the first start / 64 waves hold only their
+        // records (whole tiles when the runs are padded), the next one some.
+        // Cut them only where it pays: n whole tiles over the SIMDs end at
+        // ceil(n / simds) tiles per SIMD, thirds at ceil(3 n / simds) / 3
+        // (5,461 tiles: 6 against 5.33); at least 1.25 generations of wave
+        // slots, so a segment's predecessor has had a generation to finish
+        // (4,096 MD5 tiles cut in thirds ran 17 % slower than whole).
+        if (t == kSegKey - 1) {
+            // (rounded up: an unpadded order's wave that mixes the last long
+            // records with shorter ones is a job too -- segment 0 runs it
+            // whole, at the front of the grid; left at the back of the
+            // segmented jobs its 21 long records ran alone for 2 ms of C4.)
+            const uint64_t n = (start + 63) / 64, sm = seg_simds ? seg_simds : 1;
+            const uint64_t a0 = (n + sm - 1) / sm * sm, a3 = (kSegs * n + sm - 1) / sm * sm;
+            const bool pays = 100 * kSegs * a0 > 103 * a3 && 4 * n >= 5 * (uint64_t)seg_min;
+            misc[1] = (seg_min && seg_simds && pays) ? (uint32_t)n : 0u;
+        }
         // order position of the key's first local entry, minus its local offset
         h[t] = start + bk - loc[t];
     }
     if (blockIdx.x == 0 && t == 0) gptr(work)[kBucketNTiles] = misc[0];
     __syncthreads();
+    if (seg_min) {
+        // Every block zeroes its share of the segment flags (read by the
+        // batch kernel, next on the stream); block 0 publishes the count.
+        const uint32_t nseg = misc[1];
+        for (uint32_t i = blockIdx.x * blockDim.x + t; i < nseg; i += nb * blockDim.x)
+            gptr(seg_flags)[kSegHead + i] = 0u;
+        if (blockIdx.x == 0 && t == 0) gptr(seg_flags)[0] = nseg;
+    }
     // chunk <= kBucketChunkMax (bucket_chunk): the whole chunk sorts in LDS.
     for (uint64_t i0 = lo + t; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
         uint32_t k[kBucketUnroll];
@@ -353,7 +382,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
 }
 
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, hipStream_t s) {
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, hipStream_t s) {
     // work: [tot | spare | spare | entry count] then `order`
     // (bucket_order_words), then cnt, base (nb x kBucketKeys each) and the
     // 16-bit keys; every word the kernels read is written
@@ -369,12 +398,30 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tile
         hipLaunchKernelGGL(bucket_count_kernel<false>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, keys);
     hipLaunchKernelGGL(bucket_base_kernel, dim3((kBucketKeys + 3) / 4), dim3(256), 0, s, cnt, nb, base, work, a.bad,
                        a.check_host, a.bad_epoch);
+    if (!a.seg) seg_min = 0;
+    const uint32_t simds = 4u * (uint32_t)device_cu_count();
     if (tiles)
         hipLaunchKernelGGL(bucket_place_kernel<true>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
-                           work, order);
+                           work, order, seg_min, simds, a.seg);
     else
         hipLaunchKernelGGL(bucket_place_kernel<false>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
-                           work, order);
+                           work, order, seg_min, simds, a.seg);
+}
+
+uint32_t tile_slots(int alg) {
+    // 4 SIMDs per CU x the batch kernel's waves per SIMD: the tile kernel's,
+    // or md_lines_kernel's for SHA-384/512.
+    uint32_t occ = 0;
+    switch (alg) {
+    case 1: occ = Md5::kTileOcc; break;
+    case 2: occ = Sha1::kTileOcc; break;
+    case 3: occ = Sha256<true>::kTileOcc; break;
+    case 4: occ = Sha256<false>::kTileOcc; break;
+    case 5:
+    case 6: occ = kLinesOcc; break;
+    default: break;
+    }
+    return occ * 4u * (uint32_t)device_cu_count();
 }
 
 // ------------------------------------------------------------- dispatch

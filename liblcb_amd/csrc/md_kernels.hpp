@@ -12,6 +12,7 @@
 
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
+#include "seg_jobs.hpp"
 
 namespace lcbgpu {
 
@@ -340,12 +341,15 @@ __global__ __launch_bounds__(64 * kFixedWaves) void md_fixed_lds_kernel(KArgs a)
 #ifndef LCB_LINES128
 #define LCB_LINES128 1
 #endif
+// One-wave workgroups (as the tile kernel), kLinesOcc per SIMD.  Segmented
+// long waves (a.seg, seg_jobs.hpp): the first kSegs x nseg workgroups run
+// thirds of the first nseg waves' line loops, handing the state on.
 template <class H, bool kHmac>
-__global__ __launch_bounds__(256, 4) void md_lines_kernel(KArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[4][kSlabBytes];
+__global__ __launch_bounds__(64, kLinesOcc) void md_lines_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kSlabBytes];
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t first = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    TileSeg js;
+    const uint64_t first = seg_job(a, blockIdx.x, js) * 64;
     if (first >= a.count) return;  // wave-uniform
     const uint64_t i = first + lane;
     const bool valid = i < a.count;
@@ -372,23 +376,59 @@ __global__ __launch_bounds__(256, 4) void md_lines_kernel(KArgs a) {
     } else {
         st.init();
     }
-    if (nmin) {
+    // This job's lines [Lb, Le) of the streamed nmin.
+    uint32_t Lb = 0, Le = nmin;
+    bool suspend = false;
+    if (js.nsegs > 1) {
+        if (nmin < (uint32_t)js.nsegs + 2u) {   // too short to cut: segment 0 runs it whole
+            if (js.seg != 0) return;
+        } else {
+            bool whole = false;
+            if (js.seg > 0) {
+                if (!seg_wait(js.flag, js.seg, &whole)) return;
+                if (!whole) {
+                    Lb = nmin * js.seg / js.nsegs;
+                    seg_load(st.s, js.lane_state());
+                }
+            }
+            if (!whole && js.seg + 1 < js.nsegs) {
+                Le = nmin * (js.seg + 1) / js.nsegs;
+                suspend = true;
+            }
+        }
+    }
+    if (Le > Lb) {
         GatherLineStream ls;
-        ls.init_gather(msg, nmin - 1, lane, &slab[wv][0]);
+        ls.init_gather(msg + (uint64_t)Lb * 128, Le - Lb - 1, lane, slab);
         ls.issue_next_uniform<kGatherAux>();
-        for (uint32_t L = 0; L < nmin; ++L) {
+        for (uint32_t L = Lb; L < Le; ++L) {
 #if LCB_LANE_PRIO
-            if ((L & 15) == 0) wave_prio_left((uint64_t)(nmin - L) * 128);
+            // (not in segmented jobs: same-process A/B on C4, 20.6 -> 19.9 ms
+            // with segmenting on, and the build ran the unsegmented C4 4 %
+            // faster too, 19.6 -> 18.8: profiles/r5_c4_segs_ab.txt)
+            if (js.nsegs == 1 && ((L - Lb) & 15) == 0) wave_prio_left((uint64_t)(nmin - L) * 128);
 #endif
             uint32_t w[32];
             ls.take(w, w + 16);
-            if (L + 1 < nmin) ls.issue_next_uniform<kGatherAux>();
+            if (L + 1 < Le) ls.issue_next_uniform<kGatherAux>();
             st.compress(w);
+            if (suspend && L + 1 == Le) {   // (here, not after the loop: 4 VGPRs less at its exit)
+                seg_save(st.s, js.lane_state());
+                seg_publish(js.flag, js.seg);
+            }
         }
     }
+    if (suspend) return;
     if (!valid) return;
+    // The record's address and length read again (L2-hot) rather than held
+    // in 4 VGPRs through the line loop: the index is made opaque so the
+    // loads are not merged with the first ones.
+    uint64_t ix = idx;
+    asm volatile("" : "+v"(ix));
+    const uint8_t* msg2 = gptr(a.data) + (a.offsets ? gptr(a.offsets)[ix] : ix * a.stride);
+    const uint64_t len2 = gptr(a.lengths)[ix];
     const uint64_t done = (uint64_t)nmin * 128;
-    md_message(st, msg + done, len - done, prefix + done);
+    md_message(st, msg2 + done, len2 - done, prefix + done);
     uint32_t dw[H::kDigest / 4];
     st.digest_words(dw);
     if (kHmac) {
@@ -397,7 +437,7 @@ __global__ __launch_bounds__(256, 4) void md_lines_kernel(KArgs a) {
         md_outer(o, dw);
         o.digest_words(dw);
     }
-    store_digest<H::kDigest>(a.digests + idx * H::kDigest, dw);
+    store_digest<H::kDigest>(a.digests + ix * H::kDigest, dw);
 }
 
 }  // namespace lcbgpu
@@ -559,9 +599,9 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
     if constexpr (H::kBlock == 128 && LCB_LINES128) {
         // bucketed (unpadded order) 128-B-block batch: the streamed line loop
         if (a.order && a.lengths && !a.tile_next && a.count >= kPfMaxCount) {
-            const dim3 grid((unsigned)((a.count + 255) / 256));
-            if (hmac) hipLaunchKernelGGL((md_lines_kernel<H, true>), grid, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((md_lines_kernel<H, false>), grid, dim3(256), 0, s, a);
+            const dim3 grid((unsigned)((a.count + 63) / 64 * (a.seg ? kSegs : 1)));
+            if (hmac) hipLaunchKernelGGL((md_lines_kernel<H, true>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((md_lines_kernel<H, false>), grid, dim3(64), 0, s, a);
             return;
         }
     }

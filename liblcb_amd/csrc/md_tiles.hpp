@@ -53,6 +53,7 @@
 
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
+#include "seg_jobs.hpp"
 
 namespace lcbgpu {
 
@@ -462,8 +463,8 @@ __device__ __forceinline__ void tile_prio(uint32_t left) {
 #define LCB_TILE_A16 1
 #endif
 template <class H, int kMode, int kR, bool kA16 = false>
-__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab
-                                               LCB_TRACE(, TileTrace& tr)) {
+__device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
+                                               const TileSeg& js LCB_TRACE(, TileTrace& tr)) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
     const uint32_t sh = p32 & 3u;
     const uint32_t off = p32 & 127u;              // stream offset of the record's first byte
@@ -497,6 +498,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // The span in lines, in 64 bits (dmax - dmin of two int32 may exceed int32).
     const uint64_t span_lines = (uint64_t)((int64_t)dmax - (int64_t)dmin);
     if (!__all(near) || (span_lines + NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
+        if (js.seg != 0) return;     // segment 0 of a segmented tile runs it whole
         if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m_.K, m_.kl, 0);
         else md_message(st, r.p, r.len, m_.prefix);
         tile_finish<H, kMode>(a, st, r);
@@ -505,8 +507,11 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     const uint32_t lastc = (uint32_t)((end - 1) >> 4);
     TileGatherStream ls;
     ls.init(reinterpret_cast<const uint8_t*>(lo), (uint32_t)(dl - dmin) * 128u, m, lane, slab);
-    if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
-    else ls.issue_masked<true>(0, lastc, off >> 4);
+    auto issue0 = [&]() {
+        if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
+        else ls.issue_masked<true>(0, lastc, off >> 4);
+    };
+    if (js.seg == 0) issue0();
     // The rest of the geometry: lines wholly inside every record (min),
     // blocks of the padded (virtual) message + h (max), lines whose two
     // blocks are whole message blocks (min), whole message blocks (min).
@@ -524,7 +529,31 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         if (L >= NS) ls.issue_masked<false>(L, lastc);
         else ls.issue(L);
     };
-    const uint32_t LE = NL;   // lines streamed
+    // This job's whole-block lines [Lb, Le); a segment before the last
+    // stops there (suspend) and streams no further line.
+    uint32_t Lb = 0, Le = LF;
+    bool suspend = false;
+    // (Not in the keyed-suffix mode: its MD5 kernel is at 128 VGPRs without
+    // the segment paths; launch_ordered segments no suffix batch.)
+    constexpr bool kSegOK = LCB_TILE_SEG && kMode != kTileKeyedSuffix;
+    if (!kSegOK && js.nsegs > 1 && js.seg != 0) return;
+    if (kSegOK && js.nsegs > 1) {
+        if (LF < (uint32_t)js.nsegs + 2u) {   // too short to cut: segment 0 runs it whole
+            if (js.seg != 0) return;
+        } else {
+            bool whole = false;
+            if (js.seg > 0) {
+                if (!seg_wait(js.flag, js.seg, &whole)) return;
+                if (whole) issue0();
+                else Lb = seg_line(LF, js.seg, js.nsegs);
+            }
+            if (!whole && js.seg + 1 < js.nsegs) {
+                Le = seg_line(LF, js.seg + 1, js.nsegs);
+                suspend = true;
+            }
+        }
+    }
+    const uint32_t LE = suspend ? Le : NL;   // lines streamed
     TileKeep kp;      // the merge's keep masks (lane masks, once per tile)
     kp.init(m);
     uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
@@ -539,9 +568,22 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // rolled one despite 1.2 % fewer VALU (instruction cache), and their
     // carry copy is 0.6 % of a line's VALU (profiles/r5_tile_ab.txt).
     constexpr bool kTwoBuf = std::is_same<H, Md5>::value;
-    uint32_t L = 0;
+    // Resume: the saved state, and line Lb - 1 again for the carry.
+    auto resume = [&](uint32_t* yprev) {
+        seg_load(st.s, js.lane_state());
+        issue(Lb - 1u);
+        ls.take(yprev);
+        if (Lb < LE) issue(Lb);
+    };
+    uint32_t L = Lb;
     if constexpr (!kTwoBuf) {
-        for (; L < LF; ++L) {
+        if (Lb > 0) {
+            uint32_t y[32];
+            resume(y);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
+        }
+        for (; L < Le; ++L) {
             uint32_t y[32];
 #if LCB_TILE_PRIO
             if ((L & 15u) == 0) tile_prio(NL - L);
@@ -560,7 +602,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 #pragma unroll
             for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
         }
-    } else if (LF) {
+    } else if (Le) {
         uint32_t ya[32], yb[32];
         // Line L into y, cr = the other buffer's upper half (the carry).
         auto whole_line = [&](uint32_t Ln, uint32_t* y, uint32_t* cr) {
@@ -578,7 +620,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             tile_shift<kR, kA16>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
             tile_compress(st, w);
         };
-        {   // line 0: no carry block; its own block only when the record starts in the first half
+        if (Lb == 0) {   // line 0: no carry block; its own block only when the record starts in the first half
 #if LCB_TILE_PRIO
             tile_prio(NL);
 #endif
@@ -588,13 +630,15 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             uint32_t w[16];
             tile_shift<kR, kA16>(ya, ya + 16, sh, w);
             if (half() == 0) tile_compress(st, w);
+            L = 1;
+        } else {
+            resume(ya);
         }
-        L = 1;
-        for (; L + 1 < LF; L += 2) {
+        for (; L + 1 < Le; L += 2) {
             whole_line(L, yb, ya + 16);
             whole_line(L + 1, ya, yb + 16);
         }
-        if (L < LF) {
+        if (L < Le) {
             whole_line(L, yb, ya + 16);
             ++L;
 #pragma unroll
@@ -603,6 +647,13 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
 #pragma unroll
             for (int k = 0; k < 16; ++k) c[k] = ya[16 + k];
         }
+    }
+    if (suspend) {
+        // Hand the state on, then publish: segment seg + 1 may start.  (A
+        // failed exchange: the tile was taken over, nothing to hand on.)
+        seg_save(st.s, js.lane_state());
+        seg_publish(js.flag, js.seg);
+        return;
     }
     // The rest, line by line (tile_block: ends of messages, a keyed suffix,
     // padding, length);
@@ -646,7 +697,6 @@ template <class H, int kMode>
 __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kTileSlab];
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t t = blockIdx.x;
     // The entry count and the tile's `order` entries load together (`order`
     // covers the whole grid, bucket_order_words): three round trips to the
     // first line's issue (kernel arguments, entries, offsets and lengths)
@@ -654,7 +704,13 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // (16-B records written by the bucketing -- address, length, index --
     // save one more round trip but cost the bucketing a gather and 12 B
     // more per entry: 2 % slower on the packets, profiles/r4_tile_rec_ab.txt.)
-    uint32_t ent = gptr(a.order)[t * 64 + lane];
+    // Segmented long tiles (a.seg): the first kSegs x nseg blocks are their
+    // jobs, segment-major; the rest are the other tiles, in order.
+    TileSeg js;
+    const uint64_t t = seg_job(a, blockIdx.x, js);
+    // (the entry load stays inside `order`, which covers the unsegmented grid)
+    const uint64_t tmax = bucket_tiles_max(a.count) - 1;
+    uint32_t ent = gptr(a.order)[(t < tmax ? t : tmax) * 64 + lane];
     uint32_t norder = gptr(a.tile_next)[1];   // entries (pads included), from the bucketing
     asm volatile("" : "+v"(ent), "+s"(norder));
     const uint64_t ntiles = (norder + 63) / 64;
@@ -678,15 +734,15 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
         switch (R) {
         case 0:
             if (LCB_TILE_A16 && __all((reinterpret_cast<uintptr_t>(r.p) & 15u) == 0))
-                md_tile_stream<H, kMode, 0, true>(a, r, lane, slab LCB_TRACE(, tr));
+                md_tile_stream<H, kMode, 0, true>(a, r, lane, slab, js LCB_TRACE(, tr));
             else
-                md_tile_stream<H, kMode, 0>(a, r, lane, slab LCB_TRACE(, tr));
+                md_tile_stream<H, kMode, 0>(a, r, lane, slab, js LCB_TRACE(, tr));
             break;
-        case 1: md_tile_stream<H, kMode, 1>(a, r, lane, slab LCB_TRACE(, tr)); break;
-        case 2: md_tile_stream<H, kMode, 2>(a, r, lane, slab LCB_TRACE(, tr)); break;
-        default: md_tile_stream<H, kMode, 3>(a, r, lane, slab LCB_TRACE(, tr)); break;
+        case 1: md_tile_stream<H, kMode, 1>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+        case 2: md_tile_stream<H, kMode, 2>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+        default: md_tile_stream<H, kMode, 3>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
         }
-    } else {
+    } else if (js.seg == 0) {   // (segment 0 of a segmented tile runs it whole)
         md_tile_direct<H, kMode>(a, r);
     }
     LCB_TRACE(tr.mark(4); tr.w[6] |= t << 16; tr.w[7] = __builtin_amdgcn_s_memtime() - trc;
@@ -700,7 +756,7 @@ __host__ bool launch_tiles(const KArgs& a, hipStream_t s) {
     if constexpr (H::kTileOcc > 0) {
         // One wave per tile; the tile count is known on the device only, so
         // the grid is its upper bound (extra waves leave at once).
-        const uint64_t ntiles = (a.count + 63) / 64 + kBucketKeys;
+        const uint64_t ntiles = bucket_tiles_max(a.count) * (a.seg ? kSegs : 1);
         hipLaunchKernelGGL((md_tiles_kernel<H, kMode>), dim3((unsigned)ntiles), dim3(64), 0, s, a);
         return true;
     } else {

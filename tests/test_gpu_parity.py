@@ -539,6 +539,52 @@ def test_tiles_pad_heavy(gpu, oracle, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alg,key", [(1, None), (1, b"seg-key"), (2, None), (4, None), (6, None), (5, b"k")])
+def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
+    """Segmented long tiles (md_tiles.hpp TileSeg): a batch whose longest
+    class (32-64 KiB records) fills 1.25 generations of the tile kernel's
+    wave slots or more, and whose tile count leaves the SIMDs unevenly
+    loaded, runs each such tile as three jobs handing the state on through
+    memory.  Records of
+    32,704..40,000 bytes at every byte phase: the digests equal the same
+    batch with segmenting off (LCB_TILE_SEGS=0) and, on 400 samples, the
+    oracle.  SHA-384/512 (md_lines_kernel) segment on request only
+    (LCB_TILE_SEGS=2)."""
+    # 5.33 (MD5, 4 waves per SIMD) and 2.67 (SHA, 2) generations of wave
+    # slots, where thirds fill the SIMDs and whole tiles do not (the bucketing
+    # cuts only then: lcb_kernels.hip bucket_place_kernel)
+    tiles = 2726 if alg in (2, 3, 4) else 5456   # SHA-384/512: md_lines_kernel, 4 waves per SIMD
+    n = tiles * 64
+    rng = np.random.default_rng(60 + alg)
+    lens = rng.integers(32704, 40001, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 16, n - 1).astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 64
+    data = gpu.gen_synthetic(0x5E6 + alg, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    if alg in (5, 6):   # md_lines_kernel segments only when asked (lcb_hash_gpu.cpp launch_ordered)
+        monkeypatch.setenv("LCB_TILE_SEGS", "2")
+    seg = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
+    monkeypatch.setenv("LCB_TILE_SEGS", "0")
+    whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
+    monkeypatch.delenv("LCB_TILE_SEGS")
+    assert np.array_equal(seg, whole), alg
+    pick = np.sort(rng.choice(n, 400, replace=False))
+    parts, soff, pos = [], np.zeros(len(pick), np.uint64), 0
+    for j, i in enumerate(pick):
+        o, ln = int(offs[i]), int(lens[i])
+        parts.append(data[o:o + ln].cpu().numpy())
+        soff[j] = pos
+        pos += ln
+    host = np.concatenate(parts)
+    exp = oracle.batch(alg, host, soff, lens[pick], key=key)
+    assert np.array_equal(seg[pick], exp), alg
+    del data
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
 def test_bucketing_large_chunks(gpu, oracle):
     """ragged batches above 4M messages bucket in chunks of
     4097..8192 messages (two unrolled steps per thread, ~1,000 blocks), a

@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--alg", default="md5")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--launches", type=int, default=40)
+    ap.add_argument("--mode", default="plain",
+                    help="plain | hmac | keyed_hmac | keyed_suffix (keyed: the packet rows' 64 secrets)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     libs = {n: load(n) for n in a.libs.split(",")}
@@ -87,15 +89,33 @@ def main():
             dig = torch.empty((count, 4 if crc else DIGEST_SIZE[alg]), dtype=torch.uint8, device="cuda")
             launches = max(4, a.launches if wname in ("fixed", "r1k") else a.launches // (10 if wname == "c4" else 2))
 
+            if a.mode.startswith("keyed"):
+                from tests.golden_util import packet_key_index, packet_keys
+                keys = packet_keys()
+                blob = np.frombuffer(b"".join(keys), np.uint8).copy()
+                koff = np.zeros(len(keys), np.uint64)
+                koff[1:] = np.cumsum([len(k) for k in keys[:-1]])
+                klen = np.array([len(k) for k in keys], np.uint32)
+                kidx = torch.as_tensor(packet_key_index(count).astype(np.int32), device="cuda")
+                kmode = 1 if a.mode == "keyed_hmac" else 3
+            hkey = b"ab-inproc-hmac-key" if a.mode == "hmac" else None
+
             def run(L, k):
                 for _ in range(k):
-                    if crc:
+                    if a.mode.startswith("keyed"):
+                        rc = L.lcb_hash_batch_keyed(alg, kmode, blob.ctypes.data, koff.ctypes.data, klen.ctypes.data,
+                                                    len(keys), kidx.data_ptr(), data.data_ptr(),
+                                                    do.data_ptr() if do is not None else None,
+                                                    dl.data_ptr() if dl is not None else None, count, stride, stride,
+                                                    dig.data_ptr(), F_DEVICE, s.cuda_stream)
+                    elif crc:
                         rc = L.lcb_crc32_batch(crc, None, data.data_ptr(),
                                                do.data_ptr() if do is not None else None,
                                                dl.data_ptr() if dl is not None else None, count, stride, stride,
                                                dig.data_ptr(), F_DEVICE, s.cuda_stream)
                     else:
-                        rc = L.lcb_hash_batch(alg, None, 0, data.data_ptr(), do.data_ptr() if do is not None else None,
+                        rc = L.lcb_hash_batch(alg, hkey, len(hkey) if hkey else 0, data.data_ptr(),
+                                              do.data_ptr() if do is not None else None,
                                               dl.data_ptr() if dl is not None else None, count, stride, stride,
                                               dig.data_ptr(), F_DEVICE, s.cuda_stream)
                     if rc:
@@ -116,7 +136,7 @@ def main():
                     e1.record(s)
                     torch.cuda.synchronize()
                     res[n].append(e0.elapsed_time(e1) / launches)
-            out = {"work": wname, "alg": alg_name, "launches": launches, "rounds": a.rounds,
+            out = {"work": wname, "alg": alg_name, "mode": a.mode, "launches": launches, "rounds": a.rounds,
                    "digests_equal": same}
             if not same:
                 # A faster build with other digests is not a result: mark the

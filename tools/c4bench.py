@@ -24,6 +24,8 @@ p = argparse.ArgumentParser()
 p.add_argument("--alg", default="md5")
 p.add_argument("--reps", type=int, default=20)
 p.add_argument("--key", default=None)
+p.add_argument("--ab-segs", type=int, default=0,
+               help="N rounds alternating segmented long tiles on / off (LCB_TILE_SEGS) in this process")
 a = p.parse_args()
 fx = json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))["C4_1M_mixed"]
 n = fx["count"]
@@ -46,6 +48,30 @@ for name in a.alg.split(","):
                                    dl.data_ptr(), n, 0, 0, dig.data_ptr(), F_DEVICE, s.cuda_stream))
     for _ in range(3):
         launch()
+    if a.ab_segs:
+        res = {"on": [], "off": []}
+        for r in range(a.ab_segs):
+            for mode in (("on", "off") if r % 2 == 0 else ("off", "on")):
+                if mode == "off":
+                    os.environ["LCB_TILE_SEGS"] = "0"
+                else:
+                    os.environ.pop("LCB_TILE_SEGS", None)
+                launch()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(a.reps):
+                    launch()
+                e1.record(s)
+                torch.cuda.synchronize()
+                res[mode].append(e0.elapsed_time(e1) / a.reps)
+        os.environ.pop("LCB_TILE_SEGS", None)
+        on, off = sorted(res["on"]), sorted(res["off"])
+        print(json.dumps({"alg": name, "ab": "segmented long tiles on vs off, alternating rounds",
+                          "on_ms_median": round(on[len(on) // 2], 4), "off_ms_median": round(off[len(off) // 2], 4),
+                          "on_over_off": round(on[len(on) // 2] / off[len(off) // 2], 4),
+                          "on_ms": [round(x, 4) for x in res["on"]], "off_ms": [round(x, 4) for x in res["off"]]}),
+              flush=True)
+        continue
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
     for e0, e1 in ev:
         e0.record(s)
