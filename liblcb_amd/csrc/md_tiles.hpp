@@ -462,7 +462,11 @@ __device__ __forceinline__ void tile_prio(uint32_t left) {
 #ifndef LCB_TILE_A16
 #define LCB_TILE_A16 1
 #endif
-template <class H, int kMode, int kR, bool kA16 = false>
+// kSeg: the copy that runs segmented jobs (js.nsegs > 1); the other is
+// compiled without any segment path, as the packet tiles were before
+// segments (same-process A/B: one copy with both paths ran packets 0.5 %
+// slower).
+template <class H, int kMode, int kR, bool kA16, bool kSeg>
 __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
                                                const TileSeg& js LCB_TRACE(, TileTrace& tr)) {
     const uint32_t p32 = (uint32_t)reinterpret_cast<uintptr_t>(r.p);
@@ -498,7 +502,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // The span in lines, in 64 bits (dmax - dmin of two int32 may exceed int32).
     const uint64_t span_lines = (uint64_t)((int64_t)dmax - (int64_t)dmin);
     if (!__all(near) || (span_lines + NL + 1) * 128u >= (1ull << 32) || !__all(end != off)) {
-        if (js.seg != 0) return;     // segment 0 of a segmented tile runs it whole
+        if (kSeg && js.seg != 0) return;     // segment 0 of a segmented tile runs it whole
         if (kMode == kTileKeyedSuffix) md_message2(st, r.p, r.len, m_.K, m_.kl, 0);
         else md_message(st, r.p, r.len, m_.prefix);
         tile_finish<H, kMode>(a, st, r);
@@ -511,7 +515,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         if (__all(lastc >= 7u && off < 16u)) ls.issue(0);           // every lane's whole line 0
         else ls.issue_masked<true>(0, lastc, off >> 4);
     };
-    if (js.seg == 0) issue0();
+    if (!kSeg || js.seg == 0) issue0();
     // The rest of the geometry: lines wholly inside every record (min),
     // blocks of the padded (virtual) message + h (max), lines whose two
     // blocks are whole message blocks (min), whole message blocks (min).
@@ -535,9 +539,8 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     bool suspend = false;
     // (Not in the keyed-suffix mode: its MD5 kernel is at 128 VGPRs without
     // the segment paths; launch_ordered segments no suffix batch.)
-    constexpr bool kSegOK = LCB_TILE_SEG && kMode != kTileKeyedSuffix;
-    if (!kSegOK && js.nsegs > 1 && js.seg != 0) return;
-    if (kSegOK && js.nsegs > 1) {
+    constexpr bool kSegOK = kSeg && LCB_TILE_SEG && kMode != kTileKeyedSuffix;
+    if constexpr (kSegOK) {
         if (LF < (uint32_t)js.nsegs + 2u) {   // too short to cut: segment 0 runs it whole
             if (js.seg != 0) return;
         } else {
@@ -553,7 +556,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             }
         }
     }
-    const uint32_t LE = suspend ? Le : NL;   // lines streamed
+    const uint32_t LE = kSegOK && suspend ? Le : NL;   // lines streamed
     TileKeep kp;      // the merge's keep masks (lane masks, once per tile)
     kp.init(m);
     uint32_t c[16];   // dwords 16..31 of the previous (rotated) line: the carry
@@ -570,14 +573,16 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     constexpr bool kTwoBuf = std::is_same<H, Md5>::value;
     // Resume: the saved state, and line Lb - 1 again for the carry.
     auto resume = [&](uint32_t* yprev) {
-        seg_load(st.s, js.lane_state());
-        issue(Lb - 1u);
-        ls.take(yprev);
-        if (Lb < LE) issue(Lb);
+        if constexpr (kSegOK) {
+            seg_load(st.s, js.lane_state());
+            issue(Lb - 1u);
+            ls.take(yprev);
+            if (Lb < LE) issue(Lb);
+        }
     };
     uint32_t L = Lb;
     if constexpr (!kTwoBuf) {
-        if (Lb > 0) {
+        if (kSegOK && Lb > 0) {
             uint32_t y[32];
             resume(y);
 #pragma unroll
@@ -620,7 +625,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             tile_shift<kR, kA16>(y, y + 16, sh, w);   // block 2L - h: the rotated line's words R..R+16
             tile_compress(st, w);
         };
-        if (Lb == 0) {   // line 0: no carry block; its own block only when the record starts in the first half
+        if (!kSegOK || Lb == 0) {   // line 0: no carry block; its own block only when the record starts in the first half
 #if LCB_TILE_PRIO
             tile_prio(NL);
 #endif
@@ -648,12 +653,14 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
             for (int k = 0; k < 16; ++k) c[k] = ya[16 + k];
         }
     }
-    if (suspend) {
-        // Hand the state on, then publish: segment seg + 1 may start.  (A
-        // failed exchange: the tile was taken over, nothing to hand on.)
-        seg_save(st.s, js.lane_state());
-        seg_publish(js.flag, js.seg);
-        return;
+    if constexpr (kSegOK) {
+        if (suspend) {
+            // Hand the state on, then publish: segment seg + 1 may start.  (A
+            // failed exchange: the tile was taken over, nothing to hand on.)
+            seg_save(st.s, js.lane_state());
+            seg_publish(js.flag, js.seg);
+            return;
+        }
     }
     // The rest, line by line (tile_block: ends of messages, a keyed suffix,
     // padding, length);
@@ -683,6 +690,25 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         for (int k = 0; k < 16; ++k) c[k] = y[16 + k];
     }
     tile_finish<H, kMode>(a, st, r);
+}
+
+// One copy of the line loop per dword phase R: the block window's word
+// selection is static (no per-call dispatch and the register moves that
+// merge its cases).  kSeg: the copy for segmented jobs.
+template <class H, int kMode, bool kSeg>
+__device__ __forceinline__ void md_tile_phase(const KArgs& a, const TileRec& r, uint32_t lane, uint8_t* slab,
+                                              const TileSeg& js, uint32_t R LCB_TRACE(, TileTrace& tr)) {
+    switch (R) {
+    case 0:
+        if (LCB_TILE_A16 && __all((reinterpret_cast<uintptr_t>(r.p) & 15u) == 0))
+            md_tile_stream<H, kMode, 0, true, kSeg>(a, r, lane, slab, js LCB_TRACE(, tr));
+        else
+            md_tile_stream<H, kMode, 0, false, kSeg>(a, r, lane, slab, js LCB_TRACE(, tr));
+        break;
+    case 1: md_tile_stream<H, kMode, 1, false, kSeg>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+    case 2: md_tile_stream<H, kMode, 2, false, kSeg>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+    default: md_tile_stream<H, kMode, 3, false, kSeg>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+    }
 }
 
 // One tile per wave: the hardware dispatcher hands the tiles out in
@@ -727,22 +753,23 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
     const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
     const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
-    if (__all(Rl == R)) {
-        // One copy of the line loop per dword phase R: the block window's
-        // word selection is static (no per-call dispatch and the register
-        // moves that merge its cases).
-        switch (R) {
-        case 0:
-            if (LCB_TILE_A16 && __all((reinterpret_cast<uintptr_t>(r.p) & 15u) == 0))
-                md_tile_stream<H, kMode, 0, true>(a, r, lane, slab, js LCB_TRACE(, tr));
-            else
-                md_tile_stream<H, kMode, 0>(a, r, lane, slab, js LCB_TRACE(, tr));
-            break;
-        case 1: md_tile_stream<H, kMode, 1>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
-        case 2: md_tile_stream<H, kMode, 2>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
-        default: md_tile_stream<H, kMode, 3>(a, r, lane, slab, js LCB_TRACE(, tr)); break;
+    // (The keyed-suffix mode takes no segmented jobs: launch_ordered.)
+    constexpr bool kSegMode = kMode != kTileKeyedSuffix;
+    if (js.nsegs > 1 && (!kSegMode || !__all(Rl == R))) {
+        // a segmented tile that cannot be cut: segment 0 runs it whole
+        if (js.seg == 0) {
+            js.nsegs = 1;
+            if (__all(Rl == R)) md_tile_phase<H, kMode, false>(a, r, lane, slab, js, R LCB_TRACE(, tr));
+            else md_tile_direct<H, kMode>(a, r);
         }
-    } else if (js.seg == 0) {   // (segment 0 of a segmented tile runs it whole)
+    } else if (__all(Rl == R)) {
+        if constexpr (kSegMode) {
+            if (js.nsegs > 1) md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));
+            else md_tile_phase<H, kMode, false>(a, r, lane, slab, js, R LCB_TRACE(, tr));
+        } else {
+            md_tile_phase<H, kMode, false>(a, r, lane, slab, js, R LCB_TRACE(, tr));
+        }
+    } else {
         md_tile_direct<H, kMode>(a, r);
     }
     LCB_TRACE(tr.mark(4); tr.w[6] |= t << 16; tr.w[7] = __builtin_amdgcn_s_memtime() - trc;
