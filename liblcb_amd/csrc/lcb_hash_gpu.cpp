@@ -363,13 +363,9 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
         // call: the tests compare both forms in one process.)
         const char* ev = getenv("LCB_TILE_SEGS");
         const bool seg_off = ev && ev[0] == '0';
-        // The tile kernel (not the keyed-suffix mode) takes segmented waves.
-        // md_lines_kernel (SHA-384/512) can, and gains 15 % on batches of
-        // only long records, but C4 ran 5 % slower with them (not
-        // understood yet): LCB_TILE_SEGS=2 turns it on.
-        const bool lines_seg = ev && ev[0] == '2';
-        const bool seg_kernel =
-            tiles ? a.key_mode != kKeySuffix : lines_seg && (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
+        // The tile kernel (not the keyed-suffix mode) and md_lines_kernel
+        // (SHA-384/512, plain and HMAC) take segmented waves.
+        const bool seg_kernel = tiles ? a.key_mode != kKeySuffix : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
         const uint32_t seg_min = seg_kernel && !seg_off && bucket_seg_words(a.count) ? tile_slots(alg) : 0u;
         if (seg_min) a.seg = work + bucket_seg_offset(a.count);
         launch_bucketing(a, work, work + kBucketWork, tiles, seg_min, s);

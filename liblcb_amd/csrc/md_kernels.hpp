@@ -368,6 +368,18 @@ __global__ __launch_bounds__(64, kLinesOcc) void md_lines_kernel(KArgs a) {
         m = t < m ? t : m;
     }
     const uint32_t nmin = (uint32_t)__builtin_amdgcn_readfirstlane(m);
+    // Longest record of the wave, in lines (segmented jobs only): a wave
+    // whose streamed part is not most of its work is not cut.
+    uint32_t mx = 0;
+    if (js.nsegs > 1) {
+        mx = (uint32_t)(len >> 7);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t t = (uint32_t)__shfl_xor((int)mx, o, 64);
+            mx = t > mx ? t : mx;
+        }
+        mx = (uint32_t)__builtin_amdgcn_readfirstlane(mx);
+    }
     H st;
     uint64_t prefix = 0;
     if (kHmac) {
@@ -380,7 +392,11 @@ __global__ __launch_bounds__(64, kLinesOcc) void md_lines_kernel(KArgs a) {
     uint32_t Lb = 0, Le = nmin;
     bool suspend = false;
     if (js.nsegs > 1) {
-        if (nmin < (uint32_t)js.nsegs + 2u) {   // too short to cut: segment 0 runs it whole
+        // Too short to cut, or most of a lane's work is its per-lane tail (the
+        // wave that mixes the last long records with short ones: cut, its
+        // last segment ran 21 long records per lane, alone, behind every
+        // other job -- +3 ms on C4): segment 0 runs it whole, up front.
+        if (nmin < (uint32_t)js.nsegs + 2u || 8ull * nmin < 7ull * mx) {
             if (js.seg != 0) return;
         } else {
             bool whole = false;

@@ -541,7 +541,10 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
     // the segment paths; launch_ordered segments no suffix batch.)
     constexpr bool kSegOK = kSeg && LCB_TILE_SEG && kMode != kTileKeyedSuffix;
     if constexpr (kSegOK) {
-        if (LF < (uint32_t)js.nsegs + 2u) {   // too short to cut: segment 0 runs it whole
+        // too short to cut, or lines past the whole-block ones are much of
+        // the tile (mixed lengths: the last segment would run them behind
+        // every other job): segment 0 runs it whole, up front
+        if (LF < (uint32_t)js.nsegs + 2u || 8ull * LF < 7ull * NL) {
             if (js.seg != 0) return;
         } else {
             bool whole = false;

@@ -548,8 +548,7 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
     memory.  Records of
     32,704..40,000 bytes at every byte phase: the digests equal the same
     batch with segmenting off (LCB_TILE_SEGS=0) and, on 400 samples, the
-    oracle.  SHA-384/512 (md_lines_kernel) segment on request only
-    (LCB_TILE_SEGS=2)."""
+    oracle.  SHA-384/512 run md_lines_kernel's segmented jobs."""
     # 5.33 (MD5, 4 waves per SIMD) and 2.67 (SHA, 2) generations of wave
     # slots, where thirds fill the SIMDs and whole tiles do not (the bucketing
     # cuts only then: lcb_kernels.hip bucket_place_kernel)
@@ -563,8 +562,6 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
     data = gpu.gen_synthetic(0x5E6 + alg, total)
     do = torch.as_tensor(offs.astype(np.int64), device="cuda")
     dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
-    if alg in (5, 6):   # md_lines_kernel segments only when asked (lcb_hash_gpu.cpp launch_ordered)
-        monkeypatch.setenv("LCB_TILE_SEGS", "2")
     seg = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
     monkeypatch.setenv("LCB_TILE_SEGS", "0")
     whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
