@@ -37,36 +37,41 @@ constexpr uint64_t kSegWaitTicks = 10000000ull;
 struct TileSeg {
     uint32_t seg = 0, nsegs = 1;
     uint32_t* flag = nullptr;
-    uint32_t* state = nullptr;   // the wave's saved states (wave-uniform); lane l's at + l * kSegStateWords
-    // This lane's words, its address formed where used (not held in VGPRs
+    // The wave's saved states (wave-uniform base), word-major: word k of
+    // lane l at state[64 k + l], so each store instruction writes 256
+    // contiguous bytes (lane-major, 16-B per-lane runs, every dword store
+    // was 64 partial-sector writes: C4 wrote 7.1x its digest bytes).
+    uint32_t* state = nullptr;
+    // This lane's word 0, its address formed where used (not held in VGPRs
     // through the line loop).
     __device__ __forceinline__ uint32_t* lane_state() const {
         uint32_t ln = threadIdx.x & 63u;
         asm volatile("" : "+v"(ln));
-        return state + ln * kSegStateWords;
+        return state + ln;
     }
 };
 __device__ __forceinline__ uint32_t seg_line(uint32_t LF, uint32_t s, uint32_t n) { return 1u + (LF - 1u) * s / n; }
 // The hand-off: coherent stores, then (seg_publish) every store complete
-// before the flag; coherent loads after the flag was seen.
+// before the flag; coherent loads after the flag was seen.  p: this lane's
+// word 0; word i at p[64 i].
 template <int N>
 __device__ __forceinline__ void seg_save(const uint32_t (&s)[N], uint32_t* p) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) __hip_atomic_store(gptr(p) + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < N; ++i) __hip_atomic_store(gptr(p) + 64 * i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <int N>
 __device__ __forceinline__ void seg_load(uint32_t (&s)[N], const uint32_t* p) {
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < N; ++i)
-        s[i] = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s[i] = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <int N>
 __device__ __forceinline__ void seg_save(const uint64_t (&s)[N], uint32_t* p) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        __hip_atomic_store(gptr(p) + 2 * i, (uint32_t)s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gptr(p) + 2 * i + 1, (uint32_t)(s[i] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gptr(p) + 128 * i, (uint32_t)s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gptr(p) + 128 * i + 64, (uint32_t)(s[i] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 template <int N>
@@ -74,9 +79,9 @@ __device__ __forceinline__ void seg_load(uint64_t (&s)[N], const uint32_t* p) {
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const uint32_t lo = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + 2 * i, __ATOMIC_RELAXED,
+        const uint32_t lo = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + 128 * i, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hi = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + 2 * i + 1, __ATOMIC_RELAXED,
+        const uint32_t hi = __hip_atomic_load(const_cast<uint32_t*>(gptr(p)) + 128 * i + 64, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         s[i] = (uint64_t)lo | ((uint64_t)hi << 32);
     }
