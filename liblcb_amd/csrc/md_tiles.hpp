@@ -440,6 +440,10 @@ struct TileGatherStream {
 #ifndef LCB_TILE_PRIO
 #define LCB_TILE_PRIO 1
 #endif
+// Wave priority in segmented jobs too (md_lines_kernel runs them without).
+#ifndef LCB_TILE_SEG_PRIO
+#define LCB_TILE_SEG_PRIO 1
+#endif
 // Wave priority by remaining lines, longest remaining first (set every 16
 // lines; tiles under 128 lines stay at 0).  Among a SIMD's waves the arbiter
 // otherwise favours the oldest, so of two long tiles the younger, with more
@@ -594,7 +598,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         for (; L < Le; ++L) {
             uint32_t y[32];
 #if LCB_TILE_PRIO
-            if ((L & 15u) == 0) tile_prio(NL - L);
+            if ((!kSeg || LCB_TILE_SEG_PRIO) && (L & 15u) == 0) tile_prio(NL - L);
 #endif
             ls.take(y);
             LCB_TRACE(if (L == 0) tr.mark(2); if (L + 1 == NL) tr.mark(3);)
@@ -615,7 +619,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         // Line L into y, cr = the other buffer's upper half (the carry).
         auto whole_line = [&](uint32_t Ln, uint32_t* y, uint32_t* cr) {
 #if LCB_TILE_PRIO
-            if ((Ln & 15u) == 0) tile_prio(NL - Ln);
+            if ((!kSeg || LCB_TILE_SEG_PRIO) && (Ln & 15u) == 0) tile_prio(NL - Ln);
 #endif
             ls.take(y);
             LCB_TRACE(if (Ln + 1 == NL) tr.mark(3);)
@@ -630,7 +634,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         };
         if (!kSegOK || Lb == 0) {   // line 0: no carry block; its own block only when the record starts in the first half
 #if LCB_TILE_PRIO
-            tile_prio(NL);
+            if (!kSeg || LCB_TILE_SEG_PRIO) tile_prio(NL);
 #endif
             ls.take(ya);
             LCB_TRACE(tr.mark(2); if (NL == 1) tr.mark(3);)
