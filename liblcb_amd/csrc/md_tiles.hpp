@@ -440,9 +440,11 @@ struct TileGatherStream {
 #ifndef LCB_TILE_PRIO
 #define LCB_TILE_PRIO 1
 #endif
-// Wave priority in segmented jobs too (md_lines_kernel runs them without).
+// Segmented jobs run without the priority (equal jobs in dispatch order;
+// C4 same-process A/B: SHA-1 -1.3 %, MD5 and SHA-256 within 0.2 %,
+// profiles/r5_c4_segs_ab.txt), as in md_lines_kernel.
 #ifndef LCB_TILE_SEG_PRIO
-#define LCB_TILE_SEG_PRIO 1
+#define LCB_TILE_SEG_PRIO 0
 #endif
 // Wave priority by remaining lines, longest remaining first (set every 16
 // lines; tiles under 128 lines stay at 0).  Among a SIMD's waves the arbiter
