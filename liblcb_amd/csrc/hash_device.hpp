@@ -192,6 +192,32 @@ __device__ __forceinline__ void or_window64(const uint8_t* p, uint32_t lo, uint3
     }
 }
 
+// or_window64 for a buffer padded by at least 68 readable bytes before and
+// after the window (the device key table, lcb_hash_gpu.cpp key_table): the
+// 68-byte span is read with four 16-B loads and one dword, unconditionally,
+// instead of 17 predicated dword loads.
+__device__ __forceinline__ void or_window64_padded(const uint8_t* p, uint32_t lo, uint32_t hi, uint32_t w[16]) {
+    typedef uint32_t v4a __attribute__((ext_vector_type(4), aligned(4)));
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(ip & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const v4a v = *reinterpret_cast<const v4a*>(q + 4 * k);
+        d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+    }
+    d[16] = q[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const int b0 = (int)lo - 4 * k, b1 = (int)hi - 4 * k;
+        const uint32_t mlo = b0 <= 0 ? 0xffffffffu : (b0 >= 4 ? 0u : (0xffffffffu << (8 * b0)));
+        const uint32_t mhi = b1 >= 4 ? 0xffffffffu : (b1 <= 0 ? 0u : (0xffffffffu >> (32 - 8 * b1)));
+        w[k] |= v & mlo & mhi;
+    }
+}
+
 // Bytes [pos, pos + 64) of the virtual message V = A[0, la) || B[0, lb) as
 // raw LE words; bytes at or past la + lb are zero.  Keyed batches
 // (lcb_hash_batch_keyed) hash key || message and message || key this way

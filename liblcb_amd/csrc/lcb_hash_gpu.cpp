@@ -223,7 +223,7 @@ struct KeyCacheEntry {
     int alg = 0;
     int kind = 0;                    // LCB_HASH_KEY_* of a table, or 0: one HMAC key
     std::vector<uint8_t> sig;        // key bytes + lengths (the lookup key)
-    uint8_t* dbuf = nullptr;         // [key bytes | key offsets | key lengths | mid-states]
+    uint8_t* dbuf = nullptr;         // [pad | key bytes | key offsets | key lengths | mid-states]
     KeyTable kt;
     hipEvent_t ready = nullptr;
     hipStream_t sid = nullptr;       // stream that prepared it
@@ -262,11 +262,16 @@ static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const 
     const size_t nkeys = klen.size();
     const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = (nkeys * 4 + 15) & ~(size_t)15;
     const size_t mid_b = nkeys * 2 * kMidWords * sizeof(uint32_t);
-    // One host image of [key bytes | offsets | lengths] and ONE copy.
-    std::vector<uint8_t> img(blob_b + 2 * tab_b, 0);
-    if (!blob.empty()) memcpy(img.data(), blob.data(), blob.size());
-    memcpy(img.data() + blob_b, koff.data(), nkeys * 4);
-    memcpy(img.data() + blob_b + tab_b, klen.data(), nkeys * 4);
+    // One host image of [pad | key bytes | offsets | lengths] and ONE copy;
+    // the key bytes have >= 68 readable bytes on both sides (kKeyPad before,
+    // the tables and mid-states after: or_window64_padded reads a window's
+    // whole 68-byte span).
+    constexpr size_t kKeyPad = 128;
+    static_assert(2 * 16 + 2 * kMidWords * sizeof(uint32_t) >= 68, "readable bytes after the key bytes");
+    std::vector<uint8_t> img(kKeyPad + blob_b + 2 * tab_b, 0);
+    if (!blob.empty()) memcpy(img.data() + kKeyPad, blob.data(), blob.size());
+    memcpy(img.data() + kKeyPad + blob_b, koff.data(), nkeys * 4);
+    memcpy(img.data() + kKeyPad + blob_b + tab_b, klen.data(), nkeys * 4);
     const bool cache = g_kc.size() < kKeyCacheMax;
     uint8_t* dbuf = nullptr;
     if (cache) {
@@ -280,16 +285,16 @@ static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const 
     hipError_t e = hipMemcpyAsync(dbuf, img.data(), img.size(), hipMemcpyHostToDevice, s);
     KeyTable kt;
     kt.mode = (uint32_t)kind;
-    kt.keys = dbuf;
-    kt.key_off = reinterpret_cast<const uint32_t*>(dbuf + blob_b);
-    kt.key_len = reinterpret_cast<const uint32_t*>(dbuf + blob_b + tab_b);
+    kt.keys = dbuf + kKeyPad;
+    kt.key_off = reinterpret_cast<const uint32_t*>(dbuf + kKeyPad + blob_b);
+    kt.key_len = reinterpret_cast<const uint32_t*>(dbuf + kKeyPad + blob_b + tab_b);
     kt.nkeys = (uint32_t)nkeys;
-    kt.mid = reinterpret_cast<const uint32_t*>(dbuf + blob_b + 2 * tab_b);
+    kt.mid = reinterpret_cast<const uint32_t*>(dbuf + kKeyPad + blob_b + 2 * tab_b);
     if (e == hipSuccess) {
         if (kind == 0) {
             // One HMAC key: the key block by value (short key) or H(key) of the
             // uploaded bytes (long key), as hmac_setup always did.
-            launch_hmac_prep(alg, *kb, blob.size() > bsize(alg) ? dbuf : nullptr, blob.size(),
+            launch_hmac_prep(alg, *kb, blob.size() > bsize(alg) ? dbuf + kKeyPad : nullptr, blob.size(),
                              const_cast<uint32_t*>(kt.mid), s);
         } else if (kind != LCB_HASH_KEY_SUFFIX) {
             KArgs a;

@@ -181,7 +181,7 @@ __device__ __forceinline__ void tile_block(H& st, uint32_t b, uint32_t* w, uint6
                 const uint64_t kb = pos > len ? pos : len;       // first block byte taken from K
                 const uint32_t s0 = (uint32_t)(kb - pos);
                 const uint64_t e = pos + 64 < m.total ? pos + 64 : m.total;
-                or_window64(m.K + (kb - len) - s0, s0, (uint32_t)(e - pos), w);
+                or_window64_padded(m.K + (kb - len) - s0, s0, (uint32_t)(e - pos), w);
             }
             if (m.total >= pos && m.total < pos + 64) put_byte(w, (uint32_t)(m.total - pos), 0x80u);
         }
