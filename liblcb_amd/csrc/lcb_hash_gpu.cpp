@@ -368,9 +368,11 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
         // call: the tests compare both forms in one process.)
         const char* ev = getenv("LCB_TILE_SEGS");
         const bool seg_off = ev && ev[0] == '0';
-        // The tile kernel (not the keyed-suffix mode) and md_lines_kernel
-        // (SHA-384/512, plain and HMAC) take segmented waves.
-        const bool seg_kernel = tiles ? a.key_mode != kKeySuffix : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
+        // The tile kernel's plain MD5 / SHA-1 / SHA-256 digests (md_tiles.hpp:
+        // segmented copies cost code size) and md_lines_kernel (SHA-384/512,
+        // plain and HMAC) take segmented waves.
+        const bool seg_kernel = tiles ? a.key_mode == kKeyNone && a.mid == nullptr && (alg == 1 || alg == 2 || alg == 4)
+                                      : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
         const uint32_t seg_min = seg_kernel && !seg_off && bucket_seg_words(a.count) ? tile_slots(alg) : 0u;
         if (seg_min) a.seg = work + bucket_seg_offset(a.count);
         launch_bucketing(a, work, work + kBucketWork, tiles, seg_min, s);

@@ -443,6 +443,9 @@ struct TileGatherStream {
 // Segmented jobs run without the priority (equal jobs in dispatch order;
 // C4 same-process A/B: SHA-1 -1.3 %, MD5 and SHA-256 within 0.2 %,
 // profiles/r5_c4_segs_ab.txt), as in md_lines_kernel.
+#ifndef LCB_TILE_ONECOPY
+#define LCB_TILE_ONECOPY 0
+#endif
 #ifndef LCB_TILE_SEG_PRIO
 #define LCB_TILE_SEG_PRIO 0
 #endif
@@ -762,17 +765,25 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
     const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
     const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
-    // (The keyed-suffix mode takes no segmented jobs: launch_ordered.)
-    constexpr bool kSegMode = kMode != kTileKeyedSuffix;
-    if (js.nsegs > 1 && (!kSegMode || !__all(Rl == R))) {
-        // a segmented tile that cannot be cut: segment 0 runs it whole
-        if (js.seg == 0) {
-            js.nsegs = 1;
-            if (__all(Rl == R)) md_tile_phase<H, kMode, false>(a, r, lane, slab, js, R LCB_TRACE(, tr));
-            else md_tile_direct<H, kMode>(a, r);
-        }
-    } else if (__all(Rl == R)) {
-        if constexpr (kSegMode) {
+    // Segmented jobs: plain digests of MD5, SHA-1 and SHA-256 only
+    // (launch_ordered).  Each segmented copy of the line loop adds about as
+    // much machine code as the unsegmented one, and the code object's size
+    // showed in the headline: a library with segmented copies for every
+    // mode (33 MB) ran its first 20 timed fixed-stride steps 7 % slower than
+    // one without (18 MB), the same kernel, fresh processes alternating
+    // (profiles/r6_codesize_headline.txt).
+    constexpr bool kSegMode = kMode == kTilePlain && !std::is_same<H, Sha256<true>>::value;
+    const bool uniform = __all(Rl == R);
+    if (js.nsegs > 1 && (!kSegMode || !uniform)) {
+        // a segmented tile that cannot be cut: segment 0 runs it whole (one
+        // call site per copy below: a second one inlined the copy twice)
+        if (js.seg != 0) return;
+        js.nsegs = 1;
+    }
+    if (uniform) {
+        if constexpr (kSegMode && LCB_TILE_ONECOPY) {
+            md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));
+        } else if constexpr (kSegMode) {
             if (js.nsegs > 1) md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));
             else md_tile_phase<H, kMode, false>(a, r, lane, slab, js, R LCB_TRACE(, tr));
         } else {
