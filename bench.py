@@ -27,7 +27,11 @@ Extra fields on the JSON line:
                 (profiles/pmc_<alg>.json) when one exists for this workload;
                 valu_frac = VALU issue floor (committed SQ_INSTS_VALU count,
                 profiles/valu_counts.json, x 4 cycles on 1,024 SIMDs at
-                2.4 GHz) / kernel time
+                2.4 GHz) / kernel time; `clock` = the engine clock of the
+                timed launches themselves (ClockWindow: s_memtime /
+                s_memrealtime stamps on the launch stream around them) and
+                valu_frac_run_clock the same floor at that clock; every
+                per_alg, ragged_packets and ragged_c4 row carries its own
   cpu_baseline  the reference's own include/crypto code (oracle/_ref, built
                 from /root/reference) timed on this host's cores, rank 0, N=1
   per_alg       the same measurement for every algorithm (N=1), each with
@@ -156,25 +160,92 @@ def settle(seconds=0.4):
     del scratch
 
 
+CLOCK_SLOTS = 64          # clock-stamp workgroups: 8 per XCD
+
+
+class ClockWindow:
+    """Engine clock of the timed launches themselves:
+    a lcb_hash_gpu_clock_stamp grid is enqueued on the launch stream right
+    before the timed region (then synchronised, so the stamp is not inside
+    the wall time) and again right after its closing synchronise.  Per XCD,
+    clock = Δ s_memtime ÷ Δ s_memrealtime × 100 MHz over that window; the
+    HIP-event span of the launches over the window's real time says how much
+    of the window the kernels filled (`busy`).  `counter_residual_cycles`:
+    the largest spread, over one XCD's begin stamps, of s_memtime minus the
+    real time at that XCD's clock -- small when the XCD's workgroups read one
+    counter (the per-XCD pairing is then exact)."""
+
+    def __init__(self, stream):
+        self.sp = stream.cuda_stream
+        self.buf = torch.zeros((2, CLOCK_SLOTS, 3), dtype=torch.int64, device="cuda")
+
+    def _stamp(self, k):
+        check(lib().lcb_hash_gpu_clock_stamp(self.buf[k].data_ptr(), CLOCK_SLOTS, self.sp))
+
+    def begin(self):
+        self._stamp(0)
+        torch.cuda.synchronize()
+
+    def end(self):
+        self._stamp(1)
+        torch.cuda.synchronize()
+
+    def result(self, busy_ms=None):
+        s = self.buf.cpu().numpy().view(np.uint64)
+        clocks, resid = [], 0
+        for x in sorted(set(int(v) >> 32 for v in s[0, :, 0])):
+            b = s[0][(s[0, :, 0] >> np.uint64(32)) == x]
+            e = s[1][(s[1, :, 0] >> np.uint64(32)) == x]
+            if not len(b) or not len(e):
+                continue
+            dt = float(np.median(e[:, 1].astype(np.float64)) - np.median(b[:, 1].astype(np.float64)))
+            dr = float(np.median(e[:, 2].astype(np.float64)) - np.median(b[:, 2].astype(np.float64)))
+            if dr <= 0:
+                continue
+            f = dt / dr * 0.1                       # GHz (100 MHz real-time ticks)
+            clocks.append(f)
+            r = b[:, 1].astype(np.float64) - b[:, 2].astype(np.float64) * f * 10.0
+            resid = max(resid, float(r.max() - r.min()))
+        if not clocks:
+            return None
+        win_ms = float(np.median((s[1, :, 2].astype(np.float64) - s[0, :, 2].astype(np.float64)))) * 1e-5
+        out = {"clock_GHz": round(float(np.median(clocks)), 4), "clock_GHz_min": round(min(clocks), 4),
+               "clock_GHz_max": round(max(clocks), 4), "xcds": len(clocks), "window_ms": round(win_ms, 4),
+               "counter_residual_cycles": int(resid)}
+        if busy_ms:
+            out["busy"] = round(busy_ms / win_ms, 4) if win_ms > 0 else None
+        return out
+
+
+def valu_frac_at(vfloor_ms, clock, kms):
+    """The VALU issue floor (valu_floor_ms: at 2.4 GHz) at the clock the
+    timed launches ran at, over their kernel time."""
+    if not vfloor_ms or not clock or not clock.get("clock_GHz"):
+        return None
+    return round(vfloor_ms * (VALU_CLOCK_HZ / 1e9) / clock["clock_GHz"] / kms, 4)
+
+
 def hash_launch(alg, data, digests, count, stream, key=None):
     return lib().lcb_hash_batch(alg, key, len(key) if key else 0, data.data_ptr(), None, None, count,
                                 MSG_LEN, MSG_LEN, digests.data_ptr(), F_DEVICE, stream)
 
 
 def time_alg(alg, data, digests, count, steps, warmup, world, key=None):
-    """Returns (wall seconds for `steps` passes, max over ranks; mean kernel ms).
+    """Returns (wall seconds for `steps` passes, max over ranks; mean kernel
+    ms; this rank's engine clock over the timed launches, ClockWindow).
 
     The kernel time is the HIP-event span of the timed region on the launch
     stream divided by `steps` (back-to-back launches, so it is the average
     launch duration plus the inter-kernel gap).  Events around every launch
     add ~6 us per step on MI355X (tools/step_overhead.py), so only the two
-    ends are recorded."""
+    ends are recorded.  The clock stamps sit outside the wall-time bracket."""
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for _ in range(warmup):
         check(hash_launch(alg, data, digests, count, sp, key))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
+    cw = ClockWindow(stream)
+    cw.begin()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -188,8 +259,10 @@ def time_alg(alg, data, digests, count, steps, warmup, world, key=None):
         dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
-    kms = e0.elapsed_time(e1) / steps
-    return max_over_ranks(t, world), kms
+    cw.end()
+    span = e0.elapsed_time(e1)
+    kms = span / steps
+    return max_over_ranks(t, world), kms, cw.result(span)
 
 
 def counters_current(rec):
@@ -530,16 +603,19 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
         n = steps if alg == algs[0] else 3
         for _ in range(warmup if alg == algs[0] else 1):
             launch()
-        torch.cuda.synchronize()
+        cw = ClockWindow(stream)
+        cw.begin()
         t0 = time.perf_counter()
         for _ in range(n):
             launch()
         torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / n
+        cw.end()
         ab = total + count * (D + 12)          # bytes read once + digest + (u64 offset, u32 length)
         res = {"GiB_s": round(total / t / 2**30, 2), "ms_per_pass": round(t * 1e3, 3),
                "total_GiB": round(total / 2**30, 2), "buffers": count,
                "hbm_frac": round(ab / t / 1e9 / HBM_PEAK_GBS, 4),
+               "clock": cw.result(t * n * 1e3),
                "lengths": "{64, 1024, 65536}[mix64(seed+i) % 3]", "bucketed": True}
         if ref is not None:
             res["dod_equals_reference"] = hashlib.sha256(dig.cpu().numpy().tobytes()).hexdigest() == \
@@ -551,22 +627,30 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
     return out
 
 
-def _event_ms(launch, warmup, steps, stream):
+def _event_ms(launch, warmup, steps, stream, clock=False):
     """Mean HIP-event span per launch over `steps` back-to-back launches on
-    `stream` (events at the two ends only), after `warmup` launches."""
+    `stream` (events at the two ends only), after `warmup` launches; with
+    clock=True also the engine clock over those launches (ClockWindow)."""
     for _ in range(warmup):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cw = ClockWindow(stream) if clock else None
+    if cw:
+        cw.begin()
     torch.cuda.synchronize()
     e0.record(stream)
     for _ in range(steps):
         launch()
     e1.record(stream)
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / steps
+    span = e0.elapsed_time(e1)
+    if not cw:
+        return span / steps
+    cw.end()
+    return span / steps, cw.result(span)
 
 
-def bench_packets(warmup, steps, algs=("md5",)):
+def bench_packets(warmup, steps, algs=("md5",), ref_clock=None):
     """The network-packet shape of the reference's caller (SURVEY.md 8(f) row 1,
     VERDICT r2 item 1): 1M RADIUS-sized packets, lengths uniform 20..4096 B
     (include/proto/radius.h:576), packed back to back at byte offsets as in a
@@ -615,13 +699,19 @@ def bench_packets(warmup, steps, algs=("md5",)):
                     check(lib().lcb_hash_batch(alg, key, len(key) if key else 0, data.data_ptr(),
                                                d_offs.data_ptr(), d_lens.data_ptr(), count, 0, 0,
                                                dig.data_ptr(), F_DEVICE, stream.cuda_stream))
-            ms = _event_ms(launch, warmup, steps, stream)
+            ms, clk = _event_ms(launch, warmup, steps, stream, clock=True)
             ab = total + count * (D + 12 + (4 if mode else 0))
             name = "%s_%s" % (kind, alg_name)
             ok = hashlib.sha256(dig.cpu().numpy().tobytes()).hexdigest() == fx["full"][name]["dod"]
             res[name] = {"GiB_s": round(total / (ms * 1e-3) / 2**30, 2), "ms_per_pass": round(ms, 4),
                          "hbm_frac": round(ab / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "dod_equals_reference": ok}
+                         "clock": clk, "dod_equals_reference": ok}
+            if ref_clock and clk and clk.get("clock_GHz"):
+                # The row at the headline's clock: the
+                # same pass time scaled by this row's clock over the
+                # headline's (a VALU-issue-bound pass scales with the clock).
+                res[name]["hbm_frac_at_headline_clock"] = round(
+                    res[name]["hbm_frac"] * ref_clock / clk["clock_GHz"], 4)
         del dig
     del data, d_offs, d_lens, d_kidx
     torch.cuda.empty_cache()
@@ -808,7 +898,7 @@ def main():
     torch.cuda.synchronize()
 
     settle()
-    t, kms = time_alg(alg, data, digests, count, a.steps, a.warmup, world)
+    t, kms, clock = time_alg(alg, data, digests, count, a.steps, a.warmup, world)
     value = total * MSG_LEN * a.steps / t / 2**30
     alg_bytes = count * (MSG_LEN + D)      # read every message once + write its digest
     achieved = alg_bytes / (kms * 1e-3) / 1e9
@@ -844,7 +934,11 @@ def main():
                      "traffic": traffic, "kernel_ms": round(kms, 4),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "valu_floor_ms": round(vfloor, 4) if vfloor else None,
-                     "valu_frac": round(vfloor / kms, 4) if vfloor else None},
+                     "valu_frac": round(vfloor / kms, 4) if vfloor else None,
+                     # engine clock of the timed launches (rank 0's), and the
+                     # VALU floor at that clock
+                     "clock": clock,
+                     "valu_frac_run_clock": valu_frac_at(vfloor, clock, kms)},
     }
     from liblcb_amd._lib import LIB_PATH
     out["library_sha256_16"] = hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()[:16]
@@ -885,13 +979,14 @@ def main():
         per = {}
         for name, aid in sorted(ALG_IDS.items(), key=lambda x: x[1]):
             dg = torch.empty((count, DIGEST_SIZE[aid]), dtype=torch.uint8, device="cuda")
-            tt, km = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1)
+            tt, km, ck = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1)
             ab = count * (MSG_LEN + DIGEST_SIZE[aid])
             vf = valu_floor_ms(aid, count)
             per[name] = {"GiB_s": round(count * MSG_LEN * max(3, a.steps // 4) / tt / 2**30, 2),
                          "kernel_ms": round(km, 4),
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "valu_frac": round(vf / km, 4) if vf else None}
+                         "valu_frac": round(vf / km, 4) if vf else None,
+                         "clock": ck, "valu_frac_run_clock": valu_frac_at(vf, ck, km)}
             clk = pmc_clock_ghz(aid)
             if vf and clk:
                 # The same floor at the clock the PMC pass measured under this
@@ -918,9 +1013,10 @@ def main():
         for name in ("md5", "sha1", "sha256", "sha512"):
             aid = ALG_IDS[name]
             dg = torch.empty((count, DIGEST_SIZE[aid]), dtype=torch.uint8, device="cuda")
-            tt, km = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1, key=key)
+            tt, km, ck = time_alg(aid, data, dg, count, max(3, a.steps // 4), 10, 1, key=key)
             hm["hmac_" + name] = {"GiB_s": round(count * MSG_LEN * max(3, a.steps // 4) / tt / 2**30, 2),
-                                  "call_ms": round(km, 4), "key_bytes": len(key)}
+                                  "call_ms": round(km, 4), "key_bytes": len(key),
+                                  "clock_GHz": ck["clock_GHz"] if ck else None}
             del dg
         out["hmac"] = hm
         c4 = bench_c4([alg] + [ALG_IDS[n] for n in ("sha1", "sha256", "sha512", "gost256") if ALG_IDS[n] != alg],
@@ -945,7 +1041,8 @@ def main():
                         r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
                         blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
         out["ragged_c4_per_alg"] = c4
-        out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4))
+        out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4),
+                                              ref_clock=clock["clock_GHz"] if clock else None)
         out["crc32"] = bench_crc(data, count, max(3, a.steps // 4))
         settle()   # ChaCha20 is VALU-heavy: let the clock settle after the HBM-bound CRC launches
         out["chacha"] = bench_chacha(data, count, max(3, a.steps // 4))

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define LCB_HASH_GPU_ABI_VERSION	5
+#define LCB_HASH_GPU_ABI_VERSION	6
 
 /* Algorithm ids. */
 #define LCB_HASH_MD5		1	/* md5.h */
@@ -200,8 +200,11 @@ int	gost3411_2012_hmac_get_digest_batch(size_t bits, const uint8_t *key,
  * Device mode enables peer access from every device to devs[0] once
  * (hipDeviceEnablePeerAccess) and enqueues every remote part's copies
  * before it waits for any part; part streams and buffers are pooled per
- * device.  lcb_hash_multi_stats reports what the device-mode calls did
- * (ABI v5). */
+ * device.  A ragged (or offsets) batch is split on devs[0] itself, behind
+ * the caller's work on `stream`: the parts and each part's byte span are
+ * computed there and only they are read back (ABI v6; v5 copied every
+ * offset and length to the host).  lcb_hash_multi_stats reports what the
+ * device-mode calls did (ABI v5, host time v6). */
 int	lcb_hash_partition(const uint32_t *lengths, size_t count,
 	    uint32_t fixed_len, size_t nparts, uint64_t *first);
 int	lcb_hash_batch_multi(const int *devs, int ndev, int alg,
@@ -218,8 +221,25 @@ typedef struct lcb_hash_multi_stats_s {
 	uint64_t	peer_enabled;	/* device pairs (d -> devs[0]) with peer access on */
 	uint64_t	peer_unavailable; /* pairs where hipDeviceCanAccessPeer said no:
 					 * the runtime stages their copies */
+	uint64_t	host_ns;	/* host time of the device-mode calls from entry
+					 * until every part was enqueued (ABI v6) */
+	uint64_t	split_ns;	/* of which the split on devs[0] and its read-back */
+	uint64_t	device_splits;	/* calls split on devs[0] (ragged or offsets) */
 } lcb_hash_multi_stats_t;
 int	lcb_hash_multi_stats(lcb_hash_multi_stats_t *out);
+
+/* Key cache (ABI v6).  Key tables of keyed batches and single HMAC keys
+ * are uploaded, prepared (mid-states) and cached per device by their bytes,
+ * at most 16 entries, least recently used evicted first.  The cache holds
+ * secrets: an evicted entry's device buffer is zeroed before it is freed and
+ * its host copy wiped (the reference zeroises its pads, md5.h:337,358).
+ * lcb_hash_key_cache_flush drops and zeroes every entry (it synchronises the
+ * devices that hold one; EBUSY if a call in progress holds an entry, which
+ * then stays); lcb_hash_key_cache_entries counts the live entries.  The
+ * environment variable LCB_HASH_KEY_CACHE=0 turns the cache off: every call
+ * uploads its keys to a per-call buffer, zeroed before it is freed. */
+int	lcb_hash_key_cache_flush(void);
+size_t	lcb_hash_key_cache_entries(void);
 
 /* Synthetic input: writes bytes [start, start+n) of the stream
  * whose u64 word k (little-endian) is mix64(seed ^ k), into device memory. */
@@ -246,6 +266,24 @@ int	lcb_hash_gen_synthetic(uint64_t seed, uint64_t start, uint8_t *dev_out,
 int	lcb_hash_gpu_read_probe(int mode, const uint8_t *dev_data, size_t count,
 	    uint64_t stride, uint32_t fixed_len, uint32_t *dev_sink, void *stream);
 size_t	lcb_hash_gpu_probe_sink_words(int mode, size_t count);
+
+/* Diagnostics: engine-clock stamps (no reference
+ * counterpart).  Enqueues on `stream` a grid of `slots` one-wave workgroups
+ * (a multiple of 8, at most 4096; dealt round robin to the 8 XCDs); lane 0
+ * of workgroup b writes three uint64 to dev_out[3 b ..]: XCC_ID << 32 |
+ * HW_ID, s_memtime (shader-clock cycles) and s_memrealtime (100 MHz ticks).
+ * Two stamps around a run of kernels on the same stream give that run's
+ * engine clock per XCD (bench.py clock_window).  EINVAL on a bad shape. */
+int	lcb_hash_gpu_clock_stamp(uint64_t *dev_out, size_t slots, void *stream);
+
+/* Diagnostics (tests only): with LCB_SEG_TAKEOVER=1 in the environment, a
+ * ragged batch whose long waves are cut into segmented jobs
+ * runs those jobs in reverse segment order with no wait, so every cut wave
+ * is taken over by its last segment -- the path that keeps a job from
+ * waiting forever -- and the call synchronises and reads the waves' flags
+ * back.  out[4] = {cut waves, taken over, completed in segment order,
+ * other} of the last such batch. */
+int	lcb_hash_gpu_seg_last(uint32_t *out);
 
 /* Diagnostics: copies the 8 x 256 GOST LPS lookup table the kernels use
  * (generated from the RFC 6986 pi / A constants) to host memory `out`

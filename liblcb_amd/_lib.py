@@ -68,6 +68,10 @@ SIGNATURES = [
     ("lcb_hash_gpu_gost_table", ctypes.c_int, [c_vp]),
     ("lcb_hash_gpu_read_probe", ctypes.c_int, [ctypes.c_int, c_vp, c_sz, c_u64, c_u32, c_vp, c_vp]),
     ("lcb_hash_gpu_probe_sink_words", c_sz, [ctypes.c_int, c_sz]),
+    ("lcb_hash_gpu_clock_stamp", ctypes.c_int, [c_vp, c_sz, c_vp]),
+    ("lcb_hash_key_cache_flush", ctypes.c_int, []),
+    ("lcb_hash_key_cache_entries", c_sz, []),
+    ("lcb_hash_gpu_seg_last", ctypes.c_int, [c_vp]),
 ]
 
 
@@ -89,7 +93,7 @@ CHACHA_SIGNATURES = [("lcb_chacha_batch", ctypes.c_int, [ctypes.c_int] + _CHA),
 class MultiStats(ctypes.Structure):
     """lcb_hash_multi_stats_t (include/lcb_hash_gpu.h)."""
     _fields_ = [(n, c_u64) for n in ("calls", "remote_parts", "parts_enqueued_before_wait", "peer_enabled",
-                                     "peer_unavailable")]
+                                     "peer_unavailable", "host_ns", "split_ns", "device_splits")]
 
 
 class QueueSettings(ctypes.Structure):

@@ -16,7 +16,10 @@ __device__ __forceinline__ void msg_at(const KArgs& a, uint64_t i, uint64_t& idx
 
 __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
-    return k < a.nkeys ? k : a.nkeys - 1;   // never out of range: lcb_hash_batch_keyed checked the indices
+    // Required for memory safety: a device-mode batch with a bad index runs
+    // (only its digest stores are gated, batch_aborted); the clamp keeps its
+    // key-table and mid-state reads in bounds (md_tiles.hpp key_of).
+    return k < a.nkeys ? k : a.nkeys - 1;
 }
 
 // Message index of message i, re-derived where the digest is stored (i's

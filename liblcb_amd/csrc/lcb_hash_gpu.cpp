@@ -215,49 +215,150 @@ void stream_scratch_release(StreamScratch* e) {
 // every batch with the same table of peer secrets (radius_client.c:242,886,
 // 1025), and the upload (three pageable copies) plus the prep kernel cost
 // ~30 us of stream time per call (r5 trace).  Entries are looked up by their
-// exact bytes; at most kKeyCacheMax live per process (further tables take
-// the per-call path).  An entry is immutable once prepared; a stream other
-// than the one that prepared it waits on its `ready` event.
+// exact bytes; an entry is immutable once prepared; a stream other than the
+// one that prepared it waits on its `ready` event.
+//
+// The cache holds secrets (the key bytes on the host and the device, and the
+// ipad/opad mid-states, which are as good as the key), so:
+//  * at most kKeyCacheMax entries, least recently used evicted first;
+//  * an evicted or flushed entry's device buffer is zeroed in stream order
+//    after every use of it before it returns to the pool, and its host copy
+//    is zeroed (md5.h:337,358 zeroise the reference's pads the same way);
+//  * lcb_hash_key_cache_flush() drops every entry; LCB_HASH_KEY_CACHE=0
+//    turns the cache off (every call uploads its keys to a per-call buffer,
+//    zeroed before it is freed).
+// An entry is pinned while a call holds it (from the lookup until its batch
+// is enqueued, KeyRef); device-mode calls note the stream they used: an
+// entry only ever used on the evicting call's stream is zeroed in that
+// stream's order, any other after a device synchronisation.
 struct KeyCacheEntry {
     int dev = -1;
     int alg = 0;
     int kind = 0;                    // LCB_HASH_KEY_* of a table, or 0: one HMAC key
     std::vector<uint8_t> sig;        // key bytes + lengths (the lookup key)
     uint8_t* dbuf = nullptr;         // [pad | key bytes | key offsets | key lengths | mid-states]
+    size_t dbytes = 0;
     KeyTable kt;
     hipEvent_t ready = nullptr;
     hipStream_t sid = nullptr;       // stream that prepared it
+    uint32_t inflight = 0;           // calls between lookup and release
+    uint64_t tick = 0;               // last use (LRU)
+    std::vector<hipStream_t> users;  // streams of device-mode uses since it was prepared
+    bool many = false;               // more users than kKeyUsersMax
 };
 constexpr size_t kKeyCacheMax = 16;
+constexpr size_t kKeyUsersMax = 8;
 namespace {
 std::mutex g_kc_mu;
 std::vector<KeyCacheEntry*> g_kc;
+uint64_t g_kc_tick = 0;
+
+bool key_cache_on() {
+    const char* ev = getenv("LCB_HASH_KEY_CACHE");
+    return !(ev && ev[0] == '0');
+}
+
+void wipe_host(std::vector<uint8_t>& v) {
+    if (!v.empty()) {
+        volatile uint8_t* p = v.data();
+        for (size_t i = 0; i < v.size(); ++i) p[i] = 0;
+    }
+    v.clear();
+}
+
+// Zero and free an idle entry's device buffer (caller holds g_kc_mu).  When
+// every device-mode use was on `s` (the evicting call's stream, on the
+// entry's device), in stream order behind them; otherwise -- other streams,
+// which may be gone by now, so nothing is enqueued on them -- after a
+// synchronisation of the entry's device.
+void entry_destroy_locked(KeyCacheEntry* e, hipStream_t s, bool sync) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    bool done = false;
+    if (!sync && cur == e->dev && !e->many) {
+        bool only_s = true;
+        for (hipStream_t u : e->users) only_s = only_s && u == s;
+        if (only_s && hipMemsetAsync(e->dbuf, 0, e->dbytes, s) == hipSuccess && scratch_free(e->dbuf, s) == hipSuccess)
+            done = true;
+        (void)hipGetLastError();
+    }
+    if (!done) {
+        if (cur != e->dev) (void)hipSetDevice(e->dev);
+        (void)hipDeviceSynchronize();
+        (void)hipMemset(e->dbuf, 0, e->dbytes);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(e->dbuf);
+        (void)hipGetLastError();
+        if (cur != e->dev) (void)hipSetDevice(cur);
+    }
+    if (e->ready) (void)hipEventDestroy(e->ready);
+    wipe_host(e->sig);
+    delete e;
+}
+
+// Host copies of the secrets are wiped at exit (device memory goes with
+// the process; the runtime may be gone by then).
+struct KeyCacheAtExit {
+    ~KeyCacheAtExit() {
+        std::lock_guard<std::mutex> lk(g_kc_mu);
+        for (KeyCacheEntry* e : g_kc) wipe_host(e->sig);
+    }
+} g_kc_atexit;
 }  // namespace
 
-// The device key table of (alg, kind, keys): cached or built on `s`.  *temp
-// = a per-call buffer the caller releases with scratch_free after the batch
-// (the cache is full), else null.
+void key_release(KeyRef& r, hipStream_t s, bool async_use) {
+    if (r.temp) {
+        // per-call buffer: zeroed behind the batch that read it, then freed
+        (void)hipMemsetAsync(r.temp, 0, r.temp_bytes, s);
+        (void)scratch_free(r.temp, s);
+        (void)hipGetLastError();
+        r.temp = nullptr;
+    }
+    if (r.entry) {
+        std::lock_guard<std::mutex> lk(g_kc_mu);
+        KeyCacheEntry* e = static_cast<KeyCacheEntry*>(r.entry);
+        if (async_use && !e->many && std::find(e->users.begin(), e->users.end(), s) == e->users.end()) {
+            if (e->users.size() < kKeyUsersMax) e->users.push_back(s);
+            else e->many = true;
+        }
+        --e->inflight;
+        r.entry = nullptr;
+    }
+}
+
+// The device key table of (alg, kind, keys): cached or built on `s`; the
+// caller passes `ref` to key_release once its batch is enqueued.
 static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const std::vector<uint32_t>& koff,
                      const std::vector<uint32_t>& klen, const KeyBlock* kb, hipStream_t s, KeyTable* out,
-                     uint8_t** temp) {
-    *temp = nullptr;
+                     KeyRef* ref) {
+    *ref = KeyRef();
     int dev = 0;
     LCB_TRY(hipGetDevice(&dev));
     const hipStream_t sid = s;
     std::vector<uint8_t> sig(blob.begin(), blob.end());
     sig.insert(sig.end(), reinterpret_cast<const uint8_t*>(klen.data()),
                reinterpret_cast<const uint8_t*>(klen.data() + klen.size()));
+    struct Wipe {
+        std::vector<uint8_t>& v;
+        ~Wipe() { wipe_host(v); }
+    } wipe_sig{sig};
+    const bool use_cache = key_cache_on();
     std::lock_guard<std::mutex> lk(g_kc_mu);
-    for (KeyCacheEntry* e : g_kc) {
-        if (e->dev != dev || e->alg != alg || e->kind != kind || e->sig != sig) continue;
-        if (e->sid != sid || s == hipStreamPerThread) {
-            if (hipEventQuery(e->ready) != hipSuccess) {
-                (void)hipGetLastError();
-                LCB_TRY(hipStreamWaitEvent(s, e->ready, 0));
+    if (use_cache) {
+        for (KeyCacheEntry* e : g_kc) {
+            if (e->dev != dev || e->alg != alg || e->kind != kind || e->sig != sig) continue;
+            if (e->sid != sid || s == hipStreamPerThread) {
+                if (hipEventQuery(e->ready) != hipSuccess) {
+                    (void)hipGetLastError();
+                    LCB_TRY(hipStreamWaitEvent(s, e->ready, 0));
+                }
             }
+            e->tick = ++g_kc_tick;
+            ++e->inflight;
+            ref->entry = e;
+            *out = e->kt;
+            return 0;
         }
-        *out = e->kt;
-        return 0;
     }
     const size_t nkeys = klen.size();
     const size_t blob_b = (blob.size() + 15) & ~(size_t)15, tab_b = (nkeys * 4 + 15) & ~(size_t)15;
@@ -269,17 +370,26 @@ static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const 
     constexpr size_t kKeyPad = 128;
     static_assert(2 * 16 + 2 * kMidWords * sizeof(uint32_t) >= 68, "readable bytes after the key bytes");
     std::vector<uint8_t> img(kKeyPad + blob_b + 2 * tab_b, 0);
+    struct Wipe wipe_img{img};
     if (!blob.empty()) memcpy(img.data() + kKeyPad, blob.data(), blob.size());
     memcpy(img.data() + kKeyPad + blob_b, koff.data(), nkeys * 4);
     memcpy(img.data() + kKeyPad + blob_b + tab_b, klen.data(), nkeys * 4);
-    const bool cache = g_kc.size() < kKeyCacheMax;
-    uint8_t* dbuf = nullptr;
-    if (cache) {
-        LCB_TRY(hipMalloc(reinterpret_cast<void**>(&dbuf), img.size() + mid_b));
-    } else {
-        LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), img.size() + mid_b, s));
-        *temp = dbuf;
+    bool cache = use_cache;
+    if (cache && g_kc.size() >= kKeyCacheMax) {
+        // Evict the least recently used idle entry.
+        KeyCacheEntry* v = nullptr;
+        for (KeyCacheEntry* e : g_kc)
+            if (e->inflight == 0 && (!v || e->tick < v->tick)) v = e;
+        if (v) {
+            g_kc.erase(std::find(g_kc.begin(), g_kc.end(), v));
+            entry_destroy_locked(v, s, false);
+        } else {
+            cache = false;   // every entry is in use: this call takes the per-call path
+        }
     }
+    const size_t dbytes = img.size() + mid_b;
+    uint8_t* dbuf = nullptr;
+    LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&dbuf), dbytes, s));
     // Pageable source: the copy returns once the bytes are staged, so the
     // host image may die on return.
     hipError_t e = hipMemcpyAsync(dbuf, img.data(), img.size(), hipMemcpyHostToDevice, s);
@@ -311,40 +421,80 @@ static int key_table(int alg, int kind, const std::vector<uint8_t>& blob, const 
     }
     if (e != hipSuccess) {
         if (ready) (void)hipEventDestroy(ready);
-        if (cache) (void)hipFree(dbuf);
-        else (void)scratch_free(dbuf, s);
-        *temp = nullptr;
+        (void)hipMemsetAsync(dbuf, 0, dbytes, s);
+        (void)scratch_free(dbuf, s);
+        (void)hipGetLastError();
         return map_err(e);
     }
     if (cache) {
         KeyCacheEntry* ce = new KeyCacheEntry();
         ce->dev = dev; ce->alg = alg; ce->kind = kind; ce->sig.swap(sig);
-        ce->dbuf = dbuf; ce->kt = kt; ce->ready = ready; ce->sid = sid;
+        ce->dbuf = dbuf; ce->dbytes = dbytes; ce->kt = kt; ce->ready = ready; ce->sid = sid;
+        ce->tick = ++g_kc_tick;
+        ce->inflight = 1;
         g_kc.push_back(ce);
+        ref->entry = ce;
+    } else {
+        ref->temp = dbuf;
+        ref->temp_bytes = dbytes;
     }
     *out = kt;
     return 0;
 }
 
-// HMAC mid-states of one key on `s` (cached, see key_table).  *temp: a
-// per-call buffer to scratch_free after the batch, or null.
-int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid, uint8_t** temp) {
+// HMAC mid-states of one key on `s` (cached, see key_table); key_release
+// `ref` once the batch reading them is enqueued.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid, KeyRef* ref) {
     KeyBlock kb;
     memset(&kb, 0, sizeof(kb));
+    if (key_len > UINT32_MAX) return EINVAL;
     if (key_len <= bsize(alg) && key_len) memcpy(kb.w, key, key_len);
     std::vector<uint8_t> blob(key, key + key_len);
     std::vector<uint32_t> koff(1, 0u), klen(1, (uint32_t)key_len);
-    if (key_len > UINT32_MAX) return EINVAL;
     KeyTable kt;
-    const int rc = key_table(alg, 0, blob, koff, klen, &kb, s, &kt, temp);
+    const int rc = key_table(alg, 0, blob, koff, klen, &kb, s, &kt, ref);
+    wipe_host(blob);
+    volatile uint32_t* kw = kb.w;
+    for (int i = 0; i < 32; ++i) kw[i] = 0;
     if (rc) return rc;
     *mid = kt.mid;
     return 0;
 }
 
+// Segmented long waves of a bucketed batch: the wave capacity its scratch
+// holds (0: this batch is never segmented).  The tile kernel's plain MD5 /
+// SHA-1 / SHA-256 digests (md_tiles.hpp: segmented copies cost code size)
+// and md_lines_kernel (SHA-384/512, plain and HMAC) take segmented waves;
+// batches of other modes get no state region (every ragged
+// batch paid 64 B per message for it).  LCB_TILE_SEGS=0 in the environment
+// turns segmenting off (read per call: the tests compare both forms in one
+// process).
+static uint32_t seg_capacity(int alg, const KArgs& a) {
+    if (!a.lengths || a.order != nullptr || a.count < kBucketMinCount || a.count >= kBucketMaxCount) return 0;
+    const bool tiles = tiles_take(alg, a);
+    const bool seg_kernel = tiles ? a.key_mode == kKeyNone && a.mid == nullptr && (alg == 1 || alg == 2 || alg == 4)
+                                  : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
+    if (!seg_kernel) return 0;
+    const char* ev = getenv("LCB_TILE_SEGS");
+    if (ev && ev[0] == '0') return 0;
+    return bucket_seg_cap(a.count, tile_slots(alg));
+}
+
+// The take-over test (LCB_SEG_TAKEOVER=1, tests only): segmented jobs run in
+// reverse segment order with no wait, and after each such batch the host
+// reads its segment header (synchronising the stream) into g_seg_last.
+namespace {
+std::mutex g_seg_mu;
+uint32_t g_seg_last[4];
+}  // namespace
+static bool seg_takeover_test() {
+    const char* ev = getenv("LCB_SEG_TAKEOVER");
+    return ev && ev[0] == '1';
+}
+
 // Launch the batch kernel, bucketing a large ragged batch by length first
-// (no synchronisation).  Bucketing scratch: work_buf, else the stream's
-// scratch (ss, held by the caller), else a stream-ordered allocation.
+// (no synchronisation).  Bucketing scratch: work_buf (at least
+// ordered_words(alg, a) words), else a stream-ordered allocation.
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     uint32_t* work = nullptr;
     // The bucketing permutation holds message indices as uint32 and, padded
@@ -352,9 +502,11 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
     // key: its length, the scan and the tile count must stay below 2^32.
     if (a.lengths && a.order == nullptr && a.count >= kBucketMaxCount) return EINVAL;
     bool pooled = false;
+    bool seg_test = false;
     if (a.lengths && a.order == nullptr && a.count >= kBucketMinCount) {
-        // work: [key totals | spare | spare | entry count | order | ...]
-        const size_t bytes = bucket_words(a.count) * sizeof(uint32_t);
+        // work: [key totals | spare | spare | entry count | order | ... | segments]
+        const uint32_t cap = seg_capacity(alg, a);
+        const size_t bytes = bucket_words(a.count, cap) * sizeof(uint32_t);
         if (work_buf) {
             work = work_buf;
         } else {
@@ -362,33 +514,50 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
             pooled = true;
         }
         const bool tiles = tiles_take(alg, a);
-        // Segmented long tiles need their flags and states in the scratch
-        // (bucket_seg_words) and a batch that can fill the wave slots.
-        // (LCB_TILE_SEGS=0 in the environment turns segmenting off, read per
-        // call: the tests compare both forms in one process.)
-        const char* ev = getenv("LCB_TILE_SEGS");
-        const bool seg_off = ev && ev[0] == '0';
-        // The tile kernel's plain MD5 / SHA-1 / SHA-256 digests (md_tiles.hpp:
-        // segmented copies cost code size) and md_lines_kernel (SHA-384/512,
-        // plain and HMAC) take segmented waves.
-        const bool seg_kernel = tiles ? a.key_mode == kKeyNone && a.mid == nullptr && (alg == 1 || alg == 2 || alg == 4)
-                                      : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
-        const uint32_t seg_min = seg_kernel && !seg_off && bucket_seg_words(a.count) ? tile_slots(alg) : 0u;
-        if (seg_min) a.seg = work + bucket_seg_offset(a.count);
-        launch_bucketing(a, work, work + kBucketWork, tiles, seg_min, s);
+        const uint32_t seg_min = cap ? tile_slots(alg) : 0u;
+        if (seg_min) {
+            a.seg = work + bucket_seg_offset(a.count);
+            a.seg_cap = cap;
+            seg_test = seg_takeover_test();
+        }
+        launch_bucketing(a, work, work + kBucketWork, tiles, seg_min, seg_test, s);
         a.order = work + kBucketWork;
         if (tiles) a.tile_next = work + kBucketHead;
     }
     launch_batch(alg, a, s);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && seg_test) {
+        // {segmented waves, taken over, published by their last segment, other}
+        uint32_t nseg = 0;
+        e = hipMemcpyAsync(&nseg, a.seg, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        std::vector<uint32_t> fl(nseg ? nseg : 1);
+        if (e == hipSuccess && nseg)
+            e = hipMemcpy2DAsync(fl.data(), 4, a.seg + kSegHead + 64 * kSegStateWords, kSegBlockWords * 4, 4, nseg,
+                                 hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        uint32_t h[4] = {nseg, 0, 0, 0};
+        for (uint32_t i = 0; i < nseg && e == hipSuccess; ++i)
+            ++h[fl[i] == kSegTaken ? 1 : fl[i] == (uint32_t)kSegs - 1 ? 2 : 3];
+        std::lock_guard<std::mutex> lk(g_seg_mu);
+        memcpy(g_seg_last, h, sizeof(h));
+    }
     if (pooled) (void)scratch_free(work, s);
     return map_err(e);
 }
 
+size_t bucket_scratch_words(int alg, uint64_t count) {
+    KArgs a;
+    a.lengths = reinterpret_cast<const uint32_t*>(&a);   // any ragged plain batch of `count`
+    a.order = nullptr;
+    a.count = count < kBucketMinCount ? kBucketMinCount : count;
+    return bucket_words(a.count, seg_capacity(alg, a));
+}
+
 // Bucketing scratch words of a batch (0: not bucketed).
-static size_t ordered_words(const KArgs& a) {
+static size_t ordered_words(int alg, const KArgs& a) {
     return (a.lengths && a.order == nullptr && a.count >= kBucketMinCount && a.count < kBucketMaxCount)
-               ? bucket_words(a.count)
+               ? bucket_words(a.count, seg_capacity(alg, a))
                : 0;
 }
 
@@ -471,18 +640,19 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
         a.bad_epoch = kc->epoch;
         a.check_host = kc->fused_host;
     }
-    uint8_t* temp = nullptr;
+    KeyRef kref;
     if (key) {
         const uint32_t* mid = nullptr;
-        int rc = hmac_setup(alg, key, key_len, s, &mid, &temp);
+        int rc = hmac_setup(alg, key, key_len, s, &mid, &kref);
         if (rc) return rc;
         a.mid = mid;
     }
     int rc;
-    const size_t words = ordered_words(a);
+    const size_t words = ordered_words(alg, a);
     // A fused check needs this batch's bucketing on the keyed call's scratch.
-    if (kc && kc->fused_host && (words == 0 || kc->work_words < words)) return EINVAL;
-    if (kc && kc->work_words >= words) {
+    if (kc && kc->fused_host && (words == 0 || kc->work_words < words)) {
+        rc = EINVAL;
+    } else if (kc && kc->work_words >= words) {
         rc = launch_ordered(alg, a, s, kc->work);   // the keyed call's stream scratch
     } else if (words) {
         StreamScratch* ss = stream_scratch_acquire(s, words * sizeof(uint32_t));
@@ -491,7 +661,7 @@ int batch_device(int alg, const uint8_t* key, size_t key_len, const uint8_t* dat
     } else {
         rc = launch_ordered(alg, a, s);
     }
-    if (temp) (void)scratch_free(temp, s);
+    key_release(kref, s, true);
     return rc;
 }
 
@@ -614,11 +784,15 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     const bool dig_pinned = is_pinned(digests);
 
     const uint32_t* mid = nullptr;
-    uint8_t* temp = nullptr;
+    KeyRef kref;
     if (key) {
-        rc = hmac_setup(alg, key, key_len, S.st[0], &mid, &temp);
+        rc = hmac_setup(alg, key, key_len, S.st[0], &mid, &kref);
         if (rc) return rc;
-        LCB_TRY(hipStreamSynchronize(S.st[0]));   // mid-states visible to both streams
+        if (hipStreamSynchronize(S.st[0]) != hipSuccess) {   // mid-states visible to both streams
+            key_release(kref, S.st[0], false);
+            (void)hipStreamSynchronize(S.st[0]);
+            return EIO;
+        }
     }
 
     auto drain = [&](int b) -> int {
@@ -725,8 +899,8 @@ int batch_host(int alg, const uint8_t* key, size_t key_len, const uint8_t* data,
     }
     int rc2 = drain(0);
     int rc3 = drain(1);
-    if (temp) {  // both streams are drained: release a per-call HMAC state
-        (void)scratch_free(temp, S.st[0]);
+    if (key) {  // both streams are drained: release the HMAC state (a per-call one is zeroed)
+        key_release(kref, S.st[0], false);
         (void)hipStreamSynchronize(S.st[0]);
     }
     if (rc) return rc;
@@ -760,6 +934,7 @@ const char* lcb_hash_strerror(int error) {
     case EIO: return "HIP launch or copy failure";
     case EMSGSIZE: return "packet larger than a queue batch";
     case EAGAIN: return "no free queue staging slot";
+    case EBUSY: return "resource in use by a call in progress";
     default: return "unknown error";
     }
 }
@@ -814,8 +989,9 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     // The device key table (bytes, offsets, lengths, mid-states): cached
     // across calls with the same keys (key_table), else built on `s`.
     KeyTable kt;
-    uint8_t* temp = nullptr;
-    int rc = key_table(alg, key_mode, blob, koff, klen, nullptr, s, &kt, &temp);
+    KeyRef kref;
+    int rc = key_table(alg, key_mode, blob, koff, klen, nullptr, s, &kt, &kref);
+    wipe_host(blob);
     if (rc) return rc;
     kt.index = key_index;
     if (!dev_mode) {
@@ -823,14 +999,14 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
         rc = hipStreamSynchronize(s) == hipSuccess ? 0 : EIO;
         if (!rc) rc = batch_host(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests,
                                  nullptr, nullptr, &kt);
-        if (temp) (void)scratch_free(temp, s);
+        key_release(kref, s, false);
         (void)hipStreamSynchronize(s);
         return rc;
     }
     if (!key_index) {
         rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr,
                           &kt);
-        if (temp) (void)scratch_free(temp, s);
+        key_release(kref, s, true);
         return rc;
     }
     // Device mode with per-message key indices: an index >= nkeys is EINVAL
@@ -845,8 +1021,8 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     // key uploads, a memset, a read-back and 40 us of idle stream per keyed
     // call; an event record costs 6.5 us: profiles/r5_pkt_gaps.txt).
     KArgs probe;
-    probe.lengths = lengths; probe.order = nullptr; probe.count = count;
-    const size_t words = ordered_words(probe);
+    probe.lengths = lengths; probe.order = nullptr; probe.count = count; probe.key_mode = (uint32_t)key_mode;
+    const size_t words = ordered_words(alg, probe);
     StreamScratch* ss = stream_scratch_acquire(s, std::max<size_t>(words, 1) * sizeof(uint32_t));
     if (ss) {
         ss->epoch = (ss->epoch + 1) & 0x7fffffffu;
@@ -862,13 +1038,16 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
         } else {
             const uint32_t nblk = launch_key_check(key_index, count, (uint32_t)nkeys,
                                                    reinterpret_cast<uint32_t*>(ss->p), ss->hflag, kc.epoch, ss->ctr, s);
-            ss->ctr += nblk;
+            // The host's expected block count advances only with a launch
+            // that happened (a failed launch left it ahead for
+            // good and every later keyed call on the stream returned EIO).
             rc = map_err(hipGetLastError());
+            if (!rc) ss->ctr += nblk;
         }
         if (!rc)
             rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr,
                               &kt, &kc);
-        if (temp) (void)scratch_free(temp, s);
+        key_release(kref, s, true);
         if (!rc) {
             // Spin on the host word for a while, then poll with short sleeps;
             // a stream that has drained without the word is an error.
@@ -916,7 +1095,7 @@ int lcb_hash_batch_keyed(int alg, int key_mode, const uint8_t* keys, const uint6
     if (!rc && h_bad) rc = EINVAL;
     if (!rc) rc = batch_device(alg, nullptr, 0, data, offsets, lengths, count, stride, fixed_len, digests, s, nullptr, &kt);
     if (d_bad) (void)scratch_free(d_bad, s);
-    if (temp) (void)scratch_free(temp, s);
+    key_release(kref, s, true);
     return rc;
 }
 
@@ -1041,6 +1220,43 @@ int lcb_hash_gpu_read_probe(int mode, const uint8_t* dev_data, size_t count, uin
     }
     launch_probe(mode, a, dev_sink, reinterpret_cast<hipStream_t>(stream));
     return map_err(hipGetLastError());
+}
+
+int lcb_hash_gpu_clock_stamp(uint64_t* dev_out, size_t slots, void* stream) {
+    if (int rc = ensure_init()) return rc;
+    if (!dev_out || slots == 0 || slots > 4096 || slots % 8 || (reinterpret_cast<uintptr_t>(dev_out) & 7u))
+        return EINVAL;
+    launch_clock_stamp(dev_out, (uint32_t)slots, reinterpret_cast<hipStream_t>(stream));
+    return map_err(hipGetLastError());
+}
+
+int lcb_hash_key_cache_flush(void) {
+    if (int rc = ensure_init()) return rc;
+    std::lock_guard<std::mutex> lk(g_kc_mu);
+    int rc = 0;
+    for (size_t k = 0; k < g_kc.size();) {
+        KeyCacheEntry* e = g_kc[k];
+        if (e->inflight) {   // a call in progress holds it
+            rc = EBUSY;
+            ++k;
+            continue;
+        }
+        g_kc.erase(g_kc.begin() + k);
+        entry_destroy_locked(e, nullptr, true);
+    }
+    return rc;
+}
+
+size_t lcb_hash_key_cache_entries(void) {
+    std::lock_guard<std::mutex> lk(g_kc_mu);
+    return g_kc.size();
+}
+
+int lcb_hash_gpu_seg_last(uint32_t* out) {
+    if (!out) return EINVAL;
+    std::lock_guard<std::mutex> lk(g_seg_mu);
+    memcpy(out, g_seg_last, sizeof(g_seg_last));
+    return 0;
 }
 
 int lcb_hash_gpu_gost_table(uint64_t* out) {

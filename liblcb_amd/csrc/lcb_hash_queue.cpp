@@ -516,7 +516,7 @@ int validate(const lcb_hash_queue_settings_t& c) {
     return 0;
 }
 
-int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
+int alloc_slot(Slot& b, int alg, size_t msgs, size_t bytes, size_t D, size_t nleases) {
 #define Q_TRY(x) do { if ((x) != hipSuccess) return ENOMEM; } while (0)
     Q_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     Q_TRY(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
@@ -528,7 +528,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_data), bytes));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_off), msgs * 8));
     Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_len), msgs * 4));
-    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), bucket_words(msgs) * sizeof(uint32_t)));
+    Q_TRY(hipMalloc(reinterpret_cast<void**>(&b.d_work), bucket_scratch_words(alg, msgs) * sizeof(uint32_t)));
 #undef Q_TRY
     b.meta = new (std::nothrow) Meta[msgs];
     b.zrun = new (std::nothrow) uint8_t[msgs];
@@ -545,7 +545,7 @@ int alloc_slot(Slot& b, size_t msgs, size_t bytes, size_t D, size_t nleases) {
     if (hipMemcpyAsync(b.d_data, b.h_data, bytes, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemcpyAsync(b.d_off, b.h_off, msgs * 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
         hipMemcpyAsync(b.d_len, b.h_len, msgs * 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
-        hipMemsetAsync(b.d_work, 0, bucket_words(msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
+        hipMemsetAsync(b.d_work, 0, bucket_scratch_words(alg, msgs) * sizeof(uint32_t), b.stream) != hipSuccess ||
         hipStreamSynchronize(b.stream) != hipSuccess)
         return EIO;
     return 0;
@@ -587,7 +587,11 @@ Lease& tls_lease(uint64_t qid) {
 
 void lcb_hash_queue_s::release_all() {
     for (Slot& b : slots) free_slot(b);
-    if (mid) (void)hipFree(mid);
+    if (mid) {   // the queue's HMAC mid-states are as good as its key: zeroed first
+        (void)hipMemset(mid, 0, 2 * kMidWords * sizeof(uint32_t));
+        (void)hipDeviceSynchronize();
+        (void)hipFree(mid);
+    }
     mid = nullptr;
 }
 
@@ -628,20 +632,20 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
     const size_t nleases = (cfg.max_batch_msgs + q->lease_msgs - 1) / q->lease_msgs;
     int rc = 0;
     for (Slot& b : q->slots)
-        if ((rc = alloc_slot(b, cfg.max_batch_msgs, cfg.max_batch_bytes, q->D, nleases))) break;
+        if ((rc = alloc_slot(b, alg, cfg.max_batch_msgs, cfg.max_batch_bytes, q->D, nleases))) break;
     if (!rc && key) {
         // HMAC mid-states once per queue (the key is fixed for its lifetime).
         hipStream_t st = q->slots[0].stream;
         const uint32_t* mid = nullptr;
-        uint8_t* temp = nullptr;
-        rc = hmac_setup(alg, key, key_len, st, &mid, &temp);
+        KeyRef kref;
+        rc = hmac_setup(alg, key, key_len, st, &mid, &kref);
         if (!rc) {
             uint32_t* keep = nullptr;
             if (hipMalloc(reinterpret_cast<void**>(&keep), 2 * kMidWords * sizeof(uint32_t)) != hipSuccess ||
                 hipMemcpyAsync(keep, mid, 2 * kMidWords * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) !=
                     hipSuccess)
                 rc = ENOMEM;
-            if (temp) (void)scratch_free(temp, st);
+            key_release(kref, st, true);
             if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = EIO;
             q->mid = keep;
         }

@@ -38,9 +38,11 @@ struct KArgs {
     // count kernel checks the indices and sets *bad, the base kernel writes
     // the result to this pinned host word (no separate check kernel).
     uint32_t* check_host = nullptr;
-    // Segmented long tiles (md_tiles.hpp): per-tile flags, then the saved
-    // states (bucket_seg_words); nullptr: no tile is segmented.
+    // Segmented long tiles (md_tiles.hpp): header, then per segmented wave
+    // its saved states and flag (bucket_seg_words); nullptr: no tile is
+    // segmented.  seg_cap: the waves that may be cut (the grid's extra jobs).
     uint32_t* seg = nullptr;
+    uint32_t seg_cap = 0;
 };
 
 // True when the key-index check of this keyed batch found an index >= nkeys
@@ -126,24 +128,40 @@ constexpr int kSegs = 3;
 constexpr uint32_t kSegMinClass = 67;            // len_class: >= 512 blocks
 constexpr uint32_t kSegStateWords = 16;          // hash state words saved per lane (SHA-512: 8 x 64 bits)
 constexpr uint32_t kLinesOcc = 4;                // md_lines_kernel (SHA-384/512 ragged): waves per SIMD
-constexpr uint32_t kSegHead = 64;                // a.seg[0] = segmented waves; flags from a.seg[kSegHead]
 constexpr uint64_t kSegMinCount = 131072;        // 2 x 4 x 256 SIMD slots of 64 records
+// At most kSegMaxGens generations of the kernel's wave slots are cut (a
+// longer class loses little to whole waves: ceil(n / S) against n / S); the
+// scratch holds states for that many waves only, whatever the batch size
+// (sizing them by the message count cost 64 B per message).
+constexpr uint32_t kSegMaxGens = 4;
+// Segment header words (a.seg[..]): the segmented waves (nseg), the wait
+// before a take-over in 100-MHz ticks (0: kSegWaitTicks), 1 = jobs in
+// reverse segment order (the take-over test, LCB_SEG_TAKEOVER); then one
+// block per segmented wave: its saved states (kSegStateWords x 64 words,
+// word-major) and its flag, in a 256-B line of its own.
+constexpr uint32_t kSegHead = 64;
+enum { kSegHdrCount = 0, kSegHdrWait = 1, kSegHdrReverse = 3 };
+constexpr uint32_t kSegBlockWords = 64 * kSegStateWords + 64;
+constexpr uint32_t kSegTaken = 0x80000000u;      // a wave's flag once a job took it over (seg_jobs.hpp)
 __host__ __device__ inline uint64_t bucket_tiles_max(uint64_t count) { return (count + 63) / 64 + kBucketKeys; }
-// [count | pad to kSegHead | one flag per wave, padded to 64 | kSegStateWords
-// x 64 words per wave].
-__host__ __device__ inline uint64_t bucket_seg_state_offset(uint64_t count) {
-    return kSegHead + (bucket_tiles_max(count) + 63) / 64 * 64;
+// Segmented-wave capacity of a batch (the tile kernel's or md_lines_kernel's
+// wave slots `slots`): 0 below kSegMinCount.
+inline uint32_t bucket_seg_cap(uint64_t count, uint32_t slots) {
+    if (count < kSegMinCount || slots == 0) return 0;
+    const uint64_t cap = (uint64_t)kSegMaxGens * slots, tiles = bucket_tiles_max(count);
+    return (uint32_t)(cap < tiles ? cap : tiles);
 }
-inline size_t bucket_seg_words(uint64_t count) {
-    if (count < kSegMinCount) return 0;
-    return (size_t)(bucket_seg_state_offset(count) + bucket_tiles_max(count) * 64 * kSegStateWords);
+inline size_t bucket_seg_words(uint32_t seg_cap) {
+    return seg_cap ? (size_t)kSegHead + (size_t)seg_cap * kSegBlockWords : 0;
 }
 inline size_t bucket_seg_offset(uint64_t count) {
     const size_t w = (size_t)kBucketWork + bucket_order_words(count) + 2 * bucket_blocks(count) * kBucketKeys +
                      (count + 1) / 2;
     return (w + 63) / 64 * 64;
 }
-inline size_t bucket_words(uint64_t count) { return bucket_seg_offset(count) + bucket_seg_words(count); }
+inline size_t bucket_words(uint64_t count, uint32_t seg_cap = 0) {
+    return bucket_seg_offset(count) + bucket_seg_words(seg_cap);
+}
 
 // CRC-32 variants travel through the batch machinery as alg ids
 // kCrcAlgBase + variant (variant ids of include/lcb_crc32_gpu.h).
@@ -201,9 +219,12 @@ void crc_table_host(int variant, uint32_t* out);
 // kBucketWork words (key totals, entry count).  tiles: the tile kernel's
 // form, each key's run padded to whole tiles when the batch is large.
 // seg_min > 0 (a.seg set): segment the waves of the longest keys when there
-// are at least 1.25 x seg_min (wave slots) of them and cutting them evens
-// the SIMDs' load (a.seg[0] = their count, else 0; their flags zeroed).
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, hipStream_t s);
+// are at least 1.25 x seg_min (wave slots) and at most a.seg_cap of them
+// and cutting them evens the SIMDs' load (a.seg[0] = their count, else 0;
+// their flags zeroed).  seg_test: the take-over test (jobs in reverse
+// segment order, no wait before taking a tile over).
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min,
+                      bool seg_test, hipStream_t s);
 // The tile kernel's wave slots of alg on this device (0: no tile kernel).
 uint32_t tile_slots(int alg);
 // True when launch_batch(alg, a) runs the tile kernel on a bucketed batch:
@@ -228,6 +249,15 @@ void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s);
 // mode 2: the plain GOST kernel's LDS gathers alone (count lanes, the LPS
 // count of a fixed_len-byte message each); sink: one uint32 per lane.
 void launch_gost_lps_probe(uint64_t count, uint32_t fixed_len, uint32_t* sink, hipStream_t s);
+// lcb_hash_batch_multi device mode: the work-balanced split of a batch of
+// `count` messages into nparts (<= 64) and each part's byte span, on `s`:
+// res = [first 0..n | base 0..n-1 | end 0..n-1 | targets] (4 n + 1 words),
+// bsum: split_blocks(count) words.
+uint64_t split_chunk(uint64_t count);
+void launch_multi_split(const uint32_t* lengths, const uint64_t* offsets, uint64_t stride, uint32_t fixed_len,
+                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, hipStream_t s);
+// lcb_hash_gpu_clock_stamp: `slots` one-wave workgroups, 3 uint64 each.
+void launch_clock_stamp(uint64_t* out, uint32_t slots, hipStream_t s);
 void gost_table_host(uint64_t* out);
 
 // Shared by the C-ABI TUs (lcb_hash_gpu.cpp).
@@ -243,15 +273,27 @@ int device_cu_count();                  // compute units of the current device (
 // (the ingestion queue's slots).  Memory stays in the pool.
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 hipError_t scratch_free(void* p, hipStream_t s);
-// HMAC mid-states of one key, prepared on `s` and cached by the key's bytes
-// (lcb_hash_gpu.cpp key_table); *temp = a per-call buffer (cache full) the
-// caller releases with scratch_free after its last use, else null.
-int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid,
-               uint8_t** temp);
+// A call's hold on its device key table (lcb_hash_gpu.cpp key_table): a
+// cache entry, pinned until released, or a per-call buffer.
+struct KeyRef {
+    void* entry = nullptr;
+    uint8_t* temp = nullptr;
+    size_t temp_bytes = 0;
+};
+// Once the batch that reads the keys is enqueued on `s`: a per-call buffer
+// is zeroed and freed in stream order, a cache entry unpinned (async_use:
+// the batch reads it later on `s`, so evicting it must wait for `s`).
+void key_release(KeyRef& r, hipStream_t s, bool async_use);
+// HMAC mid-states of one key, prepared on `s` and cached by the key's bytes;
+// key_release(*ref) after the batch using them is enqueued.
+int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const uint32_t** mid, KeyRef* ref);
 // Batch kernel launch, bucketing a large ragged batch by length first.
 // work_buf: optional caller-owned device buffer of bucket_words(count)
 // uint32 for the bucketing of a ragged batch; null = stream-ordered allocation.
 int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf = nullptr);
+// Words of a work_buf that serves any ragged plain batch of alg of up to
+// `count` messages (segment states included where alg can be segmented).
+size_t bucket_scratch_words(int alg, uint64_t count);
 
 // The two batch paths of lcb_hash_batch (lcb_hash_gpu.cpp), on the current
 // device.  batch_device enqueues on `s`; batch_host stages through `stage`

@@ -100,6 +100,30 @@ void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s) {
     }
 }
 
+// ------------------------------------------------- engine-clock stamps
+// lcb_hash_gpu_clock_stamp: lane 0 of every one-wave workgroup writes
+// {XCC_ID << 32 | HW_ID, s_memtime (shader cycles), s_memrealtime (100 MHz)}
+// to out[3 b ..] (vector stores).  Two stamps launched on a stream around a
+// run of kernels give the engine clock of that run per XCD: Δ cycles ÷
+// Δ real time.  The workgroups are dealt round robin to the XCDs, so a grid
+// of 8 k puts k on each.
+__global__ __launch_bounds__(64) void clock_stamp_kernel(uint64_t* out) {
+    if (threadIdx.x != 0) return;
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    const uint64_t r = __builtin_amdgcn_s_memrealtime();
+    uint64_t* o = gptr(out) + 3ull * blockIdx.x;
+    o[0] = ((uint64_t)xcc << 32) | hw;
+    o[1] = t;
+    o[2] = r;
+}
+
+void launch_clock_stamp(uint64_t* out, uint32_t slots, hipStream_t s) {
+    hipLaunchKernelGGL(clock_stamp_kernel, dim3(slots), dim3(64), 0, s, out);
+}
+
 // ---------------------------------------------------- length bucketing
 // Ragged batches: lanes of one wavefront run until the longest lane's message
 // is done, so a random mix of 64 B and 64 KiB messages would make almost
@@ -251,7 +275,8 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
                                                             const uint32_t* cnt, const uint32_t* base,
                                                             const uint32_t* tot, const uint16_t* keys,
                                                             uint32_t* work, uint32_t* order, uint32_t seg_min,
-                                                            uint32_t seg_simds, uint32_t* seg_flags) {
+                                                            uint32_t seg_simds, uint32_t* seg_flags, uint32_t seg_cap,
+                                                            uint32_t seg_test) {
     __shared__ uint32_t h[kBucketKeys];        // run start in `order` of this block's entries, per key
     __shared__ uint32_t loc[kBucketKeys];      // local (sorted) offset per key, then the fill cursor
     __shared__ uint32_t len_s[kBucketKeys];
@@ -339,7 +364,7 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
             const uint64_t n = (start + 63) / 64, sm = seg_simds ? seg_simds : 1;
             const uint64_t a0 = (n + sm - 1) / sm * sm, a3 = (kSegs * n + sm - 1) / sm * sm;
             const bool pays = 100 * kSegs * a0 > 103 * a3 && 4 * n >= 5 * (uint64_t)seg_min;
-            misc[1] = (seg_min && seg_simds && pays) ? (uint32_t)n : 0u;
+            misc[1] = (seg_min && seg_simds && pays && n <= seg_cap) ? (uint32_t)n : 0u;
         }
         // order position of the key's first local entry, minus its local offset
         h[t] = start + bk - loc[t];
@@ -351,8 +376,11 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
         // batch kernel, next on the stream); block 0 publishes the count.
         const uint32_t nseg = misc[1];
         for (uint32_t i = blockIdx.x * blockDim.x + t; i < nseg; i += nb * blockDim.x)
-            gptr(seg_flags)[kSegHead + i] = 0u;
-        if (blockIdx.x == 0 && t == 0) gptr(seg_flags)[0] = nseg;
+            gptr(seg_flags)[kSegHead + (uint64_t)i * kSegBlockWords + 64 * kSegStateWords] = 0u;
+        if (blockIdx.x == 0 && t < 4) {
+            const uint32_t hv[4] = {nseg, seg_test ? 1u : 0u, 0u, seg_test ? 1u : 0u};
+            gptr(seg_flags)[t] = hv[t];   // kSegHdrCount, kSegHdrWait, (spare), kSegHdrReverse
+        }
     }
     // chunk <= kBucketChunkMax (bucket_chunk): the whole chunk sorts in LDS.
     for (uint64_t i0 = lo + t; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
@@ -382,7 +410,8 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
 }
 
-void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, hipStream_t s) {
+void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, bool seg_test,
+                      hipStream_t s) {
     // work: [tot | spare | spare | entry count] then `order`
     // (bucket_order_words), then cnt, base (nb x kBucketKeys each) and the
     // 16-bit keys; every word the kernels read is written
@@ -402,10 +431,10 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tile
     const uint32_t simds = 4u * (uint32_t)device_cu_count();
     if (tiles)
         hipLaunchKernelGGL(bucket_place_kernel<true>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
-                           work, order, seg_min, simds, a.seg);
+                           work, order, seg_min, simds, a.seg, a.seg_cap, seg_test ? 1u : 0u);
     else
         hipLaunchKernelGGL(bucket_place_kernel<false>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, base, work, keys,
-                           work, order, seg_min, simds, a.seg);
+                           work, order, seg_min, simds, a.seg, a.seg_cap, seg_test ? 1u : 0u);
 }
 
 uint32_t tile_slots(int alg) {
@@ -522,6 +551,164 @@ void launch_gen(uint64_t seed, uint64_t start, uint8_t* out, uint64_t n, hipStre
     if (blocks > 65536) blocks = 65536;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(256), 0, s, seed, start, out, n);
+}
+
+
+// ------------------------------------- multi-device split on the home device
+// lcb_hash_batch_multi, device mode: the work-balanced
+// split of a ragged batch (lcb_hash_partition's rule: first[p] is the first
+// message whose work midpoint, prefix + (len + 64) / 2, reaches p/N of the
+// total work) and each part's byte span [min offset, max offset + length),
+// computed where the offsets and lengths are, into `res` (uint64):
+//   [0, n]          first[0..n]
+//   [n+1, 2n]       base[p] (UINT64_MAX for an empty part)
+//   [2n+1, 3n]      end[p]
+//   [3n+1, 4n)      targets T_1..T_{n-1} (internal)
+// Three kernels: per-block work sums, one block scanning them (totals,
+// targets, initial values), then each block recomputing its messages'
+// prefixes, the part of every message (targets in LDS) and the spans (LDS
+// reduction, one global min / max per part per block).  Without lengths
+// every message costs the same: first[] is the equal-count split (as the
+// host rule) and only the spans are computed.
+constexpr uint32_t kSplitThreads = 1024;
+
+__device__ __forceinline__ uint64_t split_work(const uint32_t* lengths, uint32_t fixed_len, uint64_t i) {
+    return (uint64_t)(lengths ? gptr(lengths)[i] : fixed_len) + 64u;
+}
+
+__global__ __launch_bounds__(kSplitThreads) void split_sum_kernel(const uint32_t* lengths, uint32_t fixed_len,
+                                                                  uint64_t count, uint64_t chunk, uint64_t* bsum) {
+    __shared__ uint64_t red[kSplitThreads / 64];
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = lo + chunk < count ? lo + chunk : count;
+    uint64_t s = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSplitThreads) s += split_work(lengths, fixed_len, i);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += (uint64_t)__shfl_xor((unsigned long long)s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (uint32_t k = 0; k < kSplitThreads / 64; ++k) t += red[k];
+        gptr(bsum)[blockIdx.x] = t;
+    }
+}
+
+// One block: bsum[b] -> exclusive prefix (in place); res initialised.
+__global__ __launch_bounds__(kSplitThreads) void split_scan_kernel(uint64_t* bsum, uint32_t nb, uint64_t count,
+                                                                   uint32_t n, bool ragged, uint64_t* res) {
+    __shared__ uint64_t part[kSplitThreads];
+    const uint32_t t = threadIdx.x;
+    const uint64_t v = t < nb ? gptr(bsum)[t] : 0;   // nb <= kSplitThreads
+    part[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < kSplitThreads; d <<= 1) {   // Hillis-Steele inclusive scan
+        const uint64_t x = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    if (t < nb) gptr(bsum)[t] = part[t] - v;
+    const uint64_t W = part[kSplitThreads - 1];
+    uint64_t* r = gptr(res);
+    if (t <= n) r[t] = t == 0 ? 0 : (ragged || t == n ? count : (count / n) * t + (count % n) * t / n);
+    if (t < n) {
+        r[n + 1 + t] = ~0ull;
+        r[2 * n + 1 + t] = 0;
+    }
+    if (t >= 1 && t < n) {   // T_t = floor(W t / n), exactly: (W / n) t + (W % n) t / n
+        r[3 * n + t] = (W / n) * t + (W % n) * t / n;
+    }
+}
+
+__global__ __launch_bounds__(kSplitThreads) void split_place_kernel(const uint32_t* lengths, const uint64_t* offsets,
+                                                                    uint64_t stride, uint32_t fixed_len,
+                                                                    uint64_t count, uint64_t chunk,
+                                                                    const uint64_t* bbase, uint32_t n, uint64_t* res) {
+    __shared__ uint64_t tg[64];         // targets T_1..T_{n-1} (ragged) or first[0..n] (equal work)
+    __shared__ unsigned long long lmin[64], lmax[64];
+    __shared__ uint64_t wsum[kSplitThreads / 64];
+    __shared__ uint64_t carry_s;
+    const uint32_t t = threadIdx.x;
+    const bool ragged = lengths != nullptr;
+    uint64_t* r = gptr(res);
+    if (t < 64) {
+        tg[t] = ragged ? (t >= 1 && t < n ? r[3 * n + t] : 0) : (t <= n ? r[t] : count);
+        lmin[t] = ~0ull;
+        lmax[t] = 0;
+    }
+    if (t == 0) carry_s = gptr(bbase)[blockIdx.x];
+    __syncthreads();
+    // part of message i: ragged, the targets at or below its midpoint m;
+    // equal work, the last p with first[p] <= i
+    auto part_of = [&](uint64_t key) {
+        uint32_t p = 0;
+        for (uint32_t k = 1; k < n; ++k) p += tg[k] <= key;
+        return p;
+    };
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = lo + chunk < count ? lo + chunk : count;
+    for (uint64_t i0 = lo; i0 < hi; i0 += kSplitThreads) {
+        const uint64_t i = i0 + t;
+        const bool in = i < hi;
+        const uint64_t w = in ? split_work(lengths, fixed_len, i) : 0;
+        // block-wide inclusive scan of w (wave scan + wave totals)
+        uint64_t x = w;
+        const uint32_t lane = t & 63;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        if (lane == 63) wsum[t >> 6] = x;
+        __syncthreads();
+        uint64_t before = carry_s;
+        for (uint32_t k = 0; k < (t >> 6); ++k) before += wsum[k];
+        const uint64_t acc = before + x - w;       // work prefix of message i
+        __syncthreads();
+        if (t == kSplitThreads - 1) carry_s = before + x;
+        if (in) {
+            const uint32_t pi = part_of(ragged ? acc + w / 2 : i);
+            // first[p] = i for the parts (part(i - 1), part(i)]
+            uint32_t pp = 0;
+            if (i > 0) {
+                if (ragged) {
+                    const uint64_t wp = split_work(lengths, fixed_len, i - 1);
+                    pp = part_of(acc - wp + wp / 2);
+                } else {
+                    pp = part_of(i - 1);
+                }
+            }
+            if (ragged)
+                for (uint32_t p = pp + 1; p <= pi; ++p) r[p] = i;
+            const uint64_t off = offsets ? gptr(offsets)[i] : i * stride;
+            const uint64_t len = lengths ? gptr(lengths)[i] : fixed_len;
+            atomicMin(&lmin[pi], (unsigned long long)off);
+            atomicMax(&lmax[pi], (unsigned long long)(off + len));
+        }
+        __syncthreads();
+    }
+    if (t < n && lmin[t] != ~0ull) {
+        atomicMin(reinterpret_cast<unsigned long long*>(gptr(r) + n + 1 + t), lmin[t]);
+        atomicMax(reinterpret_cast<unsigned long long*>(gptr(r) + 2 * n + 1 + t), lmax[t]);
+    }
+}
+
+uint64_t split_chunk(uint64_t count) {
+    uint64_t c = (count + kSplitThreads - 1) / kSplitThreads;
+    if (c < 8192) c = 8192;
+    return (c + kSplitThreads - 1) / kSplitThreads * kSplitThreads;
+}
+
+void launch_multi_split(const uint32_t* lengths, const uint64_t* offsets, uint64_t stride, uint32_t fixed_len,
+                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, hipStream_t s) {
+    const uint64_t chunk = split_chunk(count);
+    const uint32_t nb = (uint32_t)((count + chunk - 1) / chunk);
+    hipLaunchKernelGGL(split_sum_kernel, dim3(nb), dim3(kSplitThreads), 0, s, lengths, fixed_len, count, chunk, bsum);
+    hipLaunchKernelGGL(split_scan_kernel, dim3(1), dim3(kSplitThreads), 0, s, bsum, nb, count, nparts,
+                       lengths != nullptr, res);
+    hipLaunchKernelGGL(split_place_kernel, dim3(nb), dim3(kSplitThreads), 0, s, lengths, offsets, stride, fixed_len,
+                       count, chunk, bsum, nparts, res);
 }
 
 }  // namespace lcbgpu

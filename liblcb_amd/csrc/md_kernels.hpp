@@ -401,7 +401,7 @@ __global__ __launch_bounds__(64, kLinesOcc) void md_lines_kernel(KArgs a) {
         } else {
             bool whole = false;
             if (js.seg > 0) {
-                if (!seg_wait(js.flag, js.seg, &whole)) return;
+                if (!seg_wait(js, &whole)) return;
                 if (!whole) {
                     Lb = nmin * js.seg / js.nsegs;
                     seg_load(st.s, js.lane_state());
@@ -615,7 +615,7 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
     if constexpr (H::kBlock == 128 && LCB_LINES128) {
         // bucketed (unpadded order) 128-B-block batch: the streamed line loop
         if (a.order && a.lengths && !a.tile_next && a.count >= kPfMaxCount) {
-            const dim3 grid((unsigned)((a.count + 63) / 64 * (a.seg ? kSegs : 1)));
+            const dim3 grid((unsigned)((a.count + 63) / 64 + (a.seg ? (uint64_t)(kSegs - 1) * a.seg_cap : 0)));
             if (hmac) hipLaunchKernelGGL((md_lines_kernel<H, true>), grid, dim3(64), 0, s, a);
             else hipLaunchKernelGGL((md_lines_kernel<H, false>), grid, dim3(64), 0, s, a);
             return;

@@ -66,11 +66,12 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// The key of message idx.  The clamp never fires: lcb_hash_batch_keyed
-// rejects an index >= nkeys with EINVAL before any batch kernel runs (host
-// mode on the host, device mode by key_index_check_kernel, lcb_kernels.hip,
-// whose flag is read before the batch is launched); it only keeps the
-// address inside the key table by construction.
+// The key of message idx.  The clamp is REQUIRED for memory safety: device
+// mode enqueues the batch right behind the index check (the check kernel,
+// or bucket_count_kernel<true>) and gates only the digest stores on its
+// flag (batch_aborted), so with a bad index the batch still runs, and the
+// clamp is what keeps its key-table and mid-state reads inside the table.
+// (Host mode rejects a bad index before any kernel runs.)
 __device__ __forceinline__ uint32_t key_of(const KArgs& a, uint64_t idx) {
     const uint32_t k = a.key_index ? gptr(a.key_index)[idx] : 0u;
     return k < a.nkeys ? k : a.nkeys - 1;
@@ -558,7 +559,7 @@ __device__ __forceinline__ void md_tile_stream(const KArgs& a, const TileRec& r,
         } else {
             bool whole = false;
             if (js.seg > 0) {
-                if (!seg_wait(js.flag, js.seg, &whole)) return;
+                if (!seg_wait(js, &whole)) return;
                 if (whole) issue0();
                 else Lb = seg_line(LF, js.seg, js.nsegs);
             }
@@ -803,7 +804,7 @@ __host__ bool launch_tiles(const KArgs& a, hipStream_t s) {
     if constexpr (H::kTileOcc > 0) {
         // One wave per tile; the tile count is known on the device only, so
         // the grid is its upper bound (extra waves leave at once).
-        const uint64_t ntiles = bucket_tiles_max(a.count) * (a.seg ? kSegs : 1);
+        const uint64_t ntiles = bucket_tiles_max(a.count) + (a.seg ? (uint64_t)(kSegs - 1) * a.seg_cap : 0);
         hipLaunchKernelGGL((md_tiles_kernel<H, kMode>), dim3((unsigned)ntiles), dim3(64), 0, s, a);
         return true;
     } else {

@@ -28,15 +28,19 @@ namespace lcbgpu {
 // (100 ms of the 100-MHz constant clock) takes the tile over -- flag
 // kSegTaken, the whole tile from line 0 -- so no dispatch order can leave
 // a wave spinning forever; the others then leave (the predecessor's
-// publish fails, later segments see kSegTaken).
+// publish fails, later segments see kSegTaken).  The take-over test
+// (LCB_SEG_TAKEOVER, launch_ordered) sets the wait to one tick and deals
+// the jobs in reverse segment order, so every cut tile's last segment
+// starts first and takes it over (each taken tile's flag stays kSegTaken,
+// which the test reads back).
 #ifndef LCB_TILE_SEG
 #define LCB_TILE_SEG 1
 #endif
-constexpr uint32_t kSegTaken = 0x80000000u;
 constexpr uint64_t kSegWaitTicks = 10000000ull;
 struct TileSeg {
     uint32_t seg = 0, nsegs = 1;
     uint32_t* flag = nullptr;
+    uint32_t wait = 0;              // ticks before a take-over
     // The wave's saved states (wave-uniform base), word-major: word k of
     // lane l at state[64 k + l], so each store instruction writes 256
     // contiguous bytes (lane-major, 16-B per-lane runs, every dword store
@@ -97,7 +101,9 @@ __device__ __forceinline__ void seg_publish(uint32_t* flag, uint32_t seg) {
 // Wait until segment s - 1 has published (true), or the tile was taken
 // over by another job (false: leave).  A wait past kSegWaitTicks takes the
 // tile over (*whole = true, returns true).
-__device__ __forceinline__ bool seg_wait(uint32_t* flag, uint32_t s, bool* whole) {
+__device__ __forceinline__ bool seg_wait(const TileSeg& js, bool* whole) {
+    uint32_t* const flag = js.flag;
+    const uint32_t s = js.seg;
     *whole = false;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -111,7 +117,7 @@ __device__ __forceinline__ bool seg_wait(uint32_t* flag, uint32_t s, bool* whole
             __hip_atomic_load(gptr(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (f == kSegTaken) return false;
         if (f >= s) return true;   // (the state is read with coherent loads: seg_load)
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kSegWaitTicks) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= js.wait) {
             // One lane exchanges (64 lanes on one word: which would win is
             // unspecified), the wave follows its result.
             int won = 0;
@@ -135,13 +141,19 @@ __device__ __forceinline__ bool seg_wait(uint32_t* flag, uint32_t s, bool* whole
 // other waves in order.  Returns the wave index; js describes the job.
 __device__ __forceinline__ uint64_t seg_job(const KArgs& a, uint64_t blk, TileSeg& js) {
     if (!a.seg) return blk;
-    const uint32_t nseg = gptr(a.seg)[0];
+    const uint32_t nseg = gptr(a.seg)[kSegHdrCount];
     if (blk < (uint64_t)kSegs * nseg) {
-        js.seg = (uint32_t)(blk / nseg);
-        const uint64_t w = blk - (uint64_t)js.seg * nseg;
+        const uint32_t sj = (uint32_t)(blk / nseg);
+        const uint64_t w = blk - (uint64_t)sj * nseg;
+        // (readfirstlane: the header words are uniform, and the line bounds
+        // derived from the segment go into SGPR operands)
+        const uint32_t rev = (uint32_t)__builtin_amdgcn_readfirstlane(gptr(a.seg)[kSegHdrReverse]);
+        js.seg = rev ? kSegs - 1u - sj : sj;
         js.nsegs = kSegs;
-        js.flag = a.seg + kSegHead + w;
-        js.state = a.seg + bucket_seg_state_offset(a.count) + w * 64 * kSegStateWords;
+        const uint32_t wt = (uint32_t)__builtin_amdgcn_readfirstlane(gptr(a.seg)[kSegHdrWait]);
+        js.wait = wt ? wt : (uint32_t)kSegWaitTicks;
+        js.state = a.seg + kSegHead + w * kSegBlockWords;
+        js.flag = js.state + 64 * kSegStateWords;
         return w;
     }
     return blk - (uint64_t)(kSegs - 1) * nseg;

@@ -29,7 +29,7 @@ def L():
 
 def test_exports_every_declared_symbol(L):
     names = declared_functions()
-    assert len(names) == 22 + 9 + 10 + 3, names   # gpu + queue + crc + chacha
+    assert len(names) == 26 + 9 + 10 + 3, names   # gpu + queue + crc + chacha
     out = subprocess.check_output(["nm", "-D", "--defined-only", SO]).decode()
     exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
     missing = [n for n in names if n not in exported]
@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol(L):
 
 
 def test_info_calls(L):
-    assert L.lcb_hash_gpu_abi_version() == 5
+    assert L.lcb_hash_gpu_abi_version() == 6
     assert [L.lcb_hash_digest_size(a) for a in range(0, 10)] == [0, 16, 20, 28, 32, 48, 64, 32, 64, 0]
     assert [L.lcb_hash_block_size(a) for a in range(1, 9)] == [64, 64, 64, 64, 128, 128, 64, 64]
     assert L.lcb_hash_strerror(errno.EINVAL) == b"invalid argument"

@@ -582,6 +582,47 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alg", [1, 2, 4, 6])
+def test_segmented_takeover(gpu, alg, monkeypatch):
+    """the take-over path of segmented jobs (seg_jobs.hpp
+    seg_wait): with LCB_SEG_TAKEOVER=1 the jobs of every cut wave run in
+    reverse segment order with no wait, so each wave's last segment starts
+    first, finds its predecessors not done and takes the wave over (flag
+    kSegTaken, the whole wave from line 0); the middle segment sees the flag
+    and leaves, the first one's publish fails.  The digests equal the same
+    batch with segmenting off, and the flags read back
+    (lcb_hash_gpu_seg_last) show the waves taken over."""
+    import ctypes
+    tiles = 2726 if alg in (2, 3, 4) else 5456
+    n = tiles * 64
+    rng = np.random.default_rng(160 + alg)
+    lens = rng.integers(32704, 40001, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 16, n - 1).astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 64
+    data = gpu.gen_synthetic(0x7A6 + alg, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    monkeypatch.setenv("LCB_TILE_SEGS", "0")
+    whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    monkeypatch.delenv("LCB_TILE_SEGS")
+    monkeypatch.setenv("LCB_SEG_TAKEOVER", "1")
+    taken = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    st = (ctypes.c_uint32 * 4)()
+    assert gpu.lib().lcb_hash_gpu_seg_last(st) == 0
+    monkeypatch.delenv("LCB_SEG_TAKEOVER")
+    nseg, ntaken, inorder, other = list(st)
+    print("alg %d: cut waves %d, taken over %d, in order %d, other %d" % (alg, nseg, ntaken, inorder, other))
+    assert np.array_equal(taken, whole), alg
+    assert nseg > 0 and ntaken >= 0.9 * nseg and inorder == 0, list(st)
+    # and the normal order again (the knob is per call)
+    again = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    assert np.array_equal(again, whole), alg
+    del data
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
 def test_bucketing_large_chunks(gpu, oracle):
     """ragged batches above 4M messages bucket in chunks of
     4097..8192 messages (two unrolled steps per thread, ~1,000 blocks), a

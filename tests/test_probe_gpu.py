@@ -66,3 +66,31 @@ def test_probe_rejects_bad_shapes(L):
     assert L.lcb_hash_gpu_read_probe(3, p, 64, 1024, 1024, q, s) == errno.EINVAL     # unknown mode
     assert L.lcb_hash_gpu_read_probe(2, p, 64, 1024, 1024, q, s) == 0                # GOST LPS chain runs
     torch.cuda.synchronize()
+
+
+def test_clock_stamp(L):
+    """lcb_hash_gpu_clock_stamp (bench.py ClockWindow): every XCD appears,
+    real time and shader cycles advance over a busy window, and the clock
+    they give lies in the MI355X's range (the engine clock tops out at
+    2.4 GHz).  Bad shapes are EINVAL."""
+    import liblcb_amd
+    import bench
+    s = torch.cuda.current_stream()
+    buf = torch.zeros((64, 3), dtype=torch.int64, device="cuda")
+    assert L.lcb_hash_gpu_clock_stamp(buf.data_ptr(), 63, s.cuda_stream) == errno.EINVAL
+    assert L.lcb_hash_gpu_clock_stamp(buf.data_ptr(), 0, s.cuda_stream) == errno.EINVAL
+    assert L.lcb_hash_gpu_clock_stamp(None, 64, s.cuda_stream) == errno.EINVAL
+    data = liblcb_amd.gen_synthetic(1, 1 << 28)
+    cw = bench.ClockWindow(s)
+    cw.begin()
+    for _ in range(40):
+        liblcb_amd.gen_synthetic(2, data.numel(), out=data)
+    torch.cuda.synchronize()
+    cw.end()
+    st = cw.buf.cpu().numpy().view(np.uint64)
+    assert len(set(int(v) >> 32 for v in st[0, :, 0])) == 8
+    assert (st[1, :, 2] > st[0, :, 2]).all() and (st[1, :, 1] > st[0, :, 1]).all()
+    r = cw.result()
+    print(r)
+    assert r["xcds"] == 8
+    assert 0.3 < r["clock_GHz_min"] <= r["clock_GHz_max"] < 2.6, r

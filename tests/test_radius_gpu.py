@@ -415,3 +415,70 @@ def test_hmac_key_cache_distinct_keys(gpu, oracle):
             alg = (1, 2, 4, 6, 7)[i % 5]
             got = gpu.hash_batch(alg, dd, offsets=do, lengths=dl, key=k).cpu().numpy()
             assert np.array_equal(got, oracle.batch(alg, data, offs, lens, key=k)), (alg, i, rep)
+
+
+@pytest.mark.gpu
+def test_key_cache_lru_flush_and_off(gpu, oracle, monkeypatch):
+    """ADVICE r5 (the key cache holds secrets): more distinct key tables than
+    the cache holds, repeated, stay right (least recently used evicted and
+    zeroed, re-prepared on return); lcb_hash_key_cache_flush drops every
+    entry; LCB_HASH_KEY_CACHE=0 adds none and stays right (per-call buffers)."""
+    import torch
+    L = gpu.lib()
+    data, offs, lens, kidx = _ragged(17, 600)
+    dd = torch.as_tensor(data, device="cuda")
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    dk = torch.as_tensor(kidx.astype(np.int32), device="cuda")
+    tables = [[k + bytes([t]) for k in KEYS] for t in range(20)]
+    for rep in range(2):
+        for t, keys in enumerate(tables):
+            got = gpu.hash_batch_keyed(1, 1, keys, dd, key_index=dk, offsets=do, lengths=dl).cpu().numpy()
+            assert np.array_equal(got, oracle.batch_keyed(1, 1, keys, data, kidx, offs, lens)), (rep, t)
+            assert L.lcb_hash_key_cache_entries() <= 16
+    assert L.lcb_hash_key_cache_entries() == 16
+    torch.cuda.synchronize()
+    assert L.lcb_hash_key_cache_flush() == 0
+    assert L.lcb_hash_key_cache_entries() == 0
+    monkeypatch.setenv("LCB_HASH_KEY_CACHE", "0")
+    for t in (0, 5):
+        got = gpu.hash_batch_keyed(4, 3, tables[t], dd, key_index=dk, offsets=do, lengths=dl).cpu().numpy()
+        assert np.array_equal(got, oracle.batch_keyed(4, 3, tables[t], data, kidx, offs, lens)), t
+        got = gpu.hash_batch(1, dd, offsets=do, lengths=dl, key=b"per-call key").cpu().numpy()
+        assert np.array_equal(got, oracle.batch(1, data, offs, lens, key=b"per-call key"))
+    assert L.lcb_hash_key_cache_entries() == 0
+
+
+@pytest.mark.gpu
+def test_keyed_unfused_check_bad_then_good(gpu, oracle):
+    """the unfused key-index check (key_index_check_kernel: a
+    fixed-stride keyed batch, and a ragged one under 4096 messages) counts
+    its blocks on a host-tracked counter; a bad index then a good one, back
+    to back on ONE stream, several times: EINVAL with no digest, then right
+    digests (a miscounted counter would make every later call EIO)."""
+    import torch
+    from liblcb_amd._lib import LcbHashError
+    n = 3000
+    data = gen_stream(0xF1, n * 128)
+    dd = torch.as_tensor(data, device="cuda")
+    kidx = (np.arange(n) % len(KEYS)).astype(np.uint32)
+    bad = kidx.copy()
+    bad[n - 7] = len(KEYS)
+    dk_good = torch.as_tensor(kidx.astype(np.int32), device="cuda")
+    dk_bad = torch.as_tensor(bad.astype(np.int32), device="cuda")
+    offs = np.arange(n, dtype=np.uint64) * 128
+    lens = (np.arange(n) % 120).astype(np.uint32)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    shapes = (("fixed", dict(count=n, stride=128, fixed_len=100), offs, np.full(n, 100, np.uint32)),
+              ("ragged", dict(offsets=do, lengths=dl), offs, lens))
+    for rep in range(3):
+        for name, shape, eo, el in shapes:
+            out = torch.full((n, 16), 0x5A, dtype=torch.uint8, device="cuda")
+            with pytest.raises(LcbHashError) as e:
+                gpu.hash_batch_keyed(1, 1, KEYS, dd, key_index=dk_bad, out=out, **shape)
+            assert e.value.errno == errno.EINVAL, (name, rep)
+            got = gpu.hash_batch_keyed(1, 1, KEYS, dd, key_index=dk_good, **shape)
+            assert np.array_equal(got.cpu().numpy(), oracle.batch_keyed(1, 1, KEYS, data, kidx, eo, el)), (name, rep)
+            torch.cuda.synchronize()
+            assert (out.cpu().numpy() == 0x5A).all(), (name, rep)

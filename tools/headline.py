@@ -29,6 +29,6 @@ torch.cuda.synchronize()
 out = []
 for _ in range(a.reps):
     bench.settle()
-    t, kms = bench.time_alg(1, data, dig, count, a.steps, a.warmup, 1)
+    t, kms, _clk = bench.time_alg(1, data, dig, count, a.steps, a.warmup, 1)
     out.append((round(t / a.steps * 1e3, 4), round(kms, 4)))
 print(json.dumps({"lib": os.environ.get("LCB_HASH_GPU_LIB", "product"), "ms_per_step_wall_event": out}), flush=True)
