@@ -160,20 +160,23 @@ def settle(seconds=0.4):
     del scratch
 
 
-CLOCK_SLOTS = 64          # clock-stamp workgroups: 8 per XCD
+CLOCK_SLOTS = 4096        # clock-stamp workgroups: ~16 per CU, so every CU stamps in both grids
 
 
 class ClockWindow:
     """Engine clock of the timed launches themselves:
     a lcb_hash_gpu_clock_stamp grid is enqueued on the launch stream right
     before the timed region (then synchronised, so the stamp is not inside
-    the wall time) and again right after its closing synchronise.  Per XCD,
-    clock = Δ s_memtime ÷ Δ s_memrealtime × 100 MHz over that window; the
-    HIP-event span of the launches over the window's real time says how much
-    of the window the kernels filled (`busy`).  `counter_residual_cycles`:
-    the largest spread, over one XCD's begin stamps, of s_memtime minus the
-    real time at that XCD's clock -- small when the XCD's workgroups read one
-    counter (the per-XCD pairing is then exact)."""
+    the wall time) and again right after its closing synchronise.  s_memtime
+    is a per-CU shader-cycle counter (the CUs' counters differ by arbitrary
+    offsets; s_memrealtime is one 100 MHz clock for the chip), so the stamps
+    are paired per CU (XCC_ID and HW_ID's CU / SH / SE fields): per CU,
+    clock = Δ s_memtime ÷ Δ s_memrealtime × 100 MHz over the window; the
+    median over CUs is `clock_GHz` (min / max beside it).  The HIP-event span
+    of the launches over the window's real time says how much of the window
+    the kernels filled (`busy`).  `counter_residual_cycles`: the largest
+    spread of one CU's begin stamps after removing the real time at its
+    clock (small: the CU's stamps read one counter)."""
 
     def __init__(self, stream):
         self.sp = stream.cuda_stream
@@ -190,28 +193,34 @@ class ClockWindow:
         self._stamp(1)
         torch.cuda.synchronize()
 
+    @staticmethod
+    def _by_cu(rows):
+        key = ((rows[:, 0] >> np.uint64(32)) << np.uint64(8)) | ((rows[:, 0] >> np.uint64(8)) & np.uint64(0xFF))
+        out = {}
+        for k in np.unique(key):
+            out[int(k)] = rows[key == k]
+        return out
+
     def result(self, busy_ms=None):
         s = self.buf.cpu().numpy().view(np.uint64)
-        clocks, resid = [], 0
-        for x in sorted(set(int(v) >> 32 for v in s[0, :, 0])):
-            b = s[0][(s[0, :, 0] >> np.uint64(32)) == x]
-            e = s[1][(s[1, :, 0] >> np.uint64(32)) == x]
-            if not len(b) or not len(e):
+        b, e = self._by_cu(s[0]), self._by_cu(s[1])
+        clocks, xcds, resid = [], set(), 0.0
+        for k in sorted(set(b) & set(e)):
+            bt, br = np.median(b[k][:, 1].astype(np.float64)), np.median(b[k][:, 2].astype(np.float64))
+            et, er = np.median(e[k][:, 1].astype(np.float64)), np.median(e[k][:, 2].astype(np.float64))
+            if er <= br or et <= bt:
                 continue
-            dt = float(np.median(e[:, 1].astype(np.float64)) - np.median(b[:, 1].astype(np.float64)))
-            dr = float(np.median(e[:, 2].astype(np.float64)) - np.median(b[:, 2].astype(np.float64)))
-            if dr <= 0:
-                continue
-            f = dt / dr * 0.1                       # GHz (100 MHz real-time ticks)
+            f = (et - bt) / (er - br) * 0.1          # GHz (100 MHz real-time ticks)
             clocks.append(f)
-            r = b[:, 1].astype(np.float64) - b[:, 2].astype(np.float64) * f * 10.0
+            xcds.add(k >> 8)
+            r = b[k][:, 1].astype(np.float64) - b[k][:, 2].astype(np.float64) * f * 10.0
             resid = max(resid, float(r.max() - r.min()))
         if not clocks:
             return None
-        win_ms = float(np.median((s[1, :, 2].astype(np.float64) - s[0, :, 2].astype(np.float64)))) * 1e-5
+        win_ms = float(np.median(s[1, :, 2].astype(np.float64)) - np.median(s[0, :, 2].astype(np.float64))) * 1e-5
         out = {"clock_GHz": round(float(np.median(clocks)), 4), "clock_GHz_min": round(min(clocks), 4),
-               "clock_GHz_max": round(max(clocks), 4), "xcds": len(clocks), "window_ms": round(win_ms, 4),
-               "counter_residual_cycles": int(resid)}
+               "clock_GHz_max": round(max(clocks), 4), "cus": len(clocks), "xcds": len(xcds),
+               "window_ms": round(win_ms, 4), "counter_residual_cycles": int(resid)}
         if busy_ms:
             out["busy"] = round(busy_ms / win_ms, 4) if win_ms > 0 else None
         return out
@@ -819,9 +828,10 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
         # each run attributes its own latency tail: first
         # packet -> seal, seal -> enqueued, GPU, callbacks, longest blocked
         # submit; where the worst packet sat in the run; blocked submits.
-        return {k: r.get(k) for k in ("max_fill_us", "max_launch_us", "max_gpu_us", "max_callback_us",
-                                      "max_submit_wait_us", "submit_waits", "worst_at", "lat_us_max",
-                                      "late_half_p99")}
+        # The slowest launch's own steps ride along.
+        return {k: r.get(k) for k in ("max_fill_us", "max_launch_us", "max_launch_steps_us", "max_gpu_us",
+                                      "max_callback_us", "max_submit_wait_us", "submit_waits", "worst_at",
+                                      "lat_us_max", "late_half_p99")}
     return {"packets_per_s": sat["packets_per_s"], "GiB_s": sat["GiB_s"], "batches": sat["batches"],
             # Zero-copy submit (LCB_HASH_Q_F_ZEROCOPY): packets already in a
             # registered page-locked pool (the io_buf receive buffers,
@@ -836,6 +846,7 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
             "saturated_lat_us_p50": sat["lat_us_p50"], "saturated_lat_us_p99": sat["lat_us_p99"],
             "half_load_packets_per_s": half["packets_per_s"], "half_load_lat_us_p50": half["lat_us_p50"],
             "half_load_lat_us_p99": half["lat_us_p99"], "half_load_lat_us_p999": half["lat_us_p999"],
+            "zerocopy_half_load_lat_us_p999": zc_half["lat_us_p999"],
             "half_load_lat_us_max": half["lat_us_max"], "threads": threads, "packet_bytes": MSG_LEN,
             "settings": "64K packets / 64 MiB / 200 us / 4 slots", "copy_only_GiB_s": copy["GiB_s"],
             "path": "producer memcpy into pinned lease -> H2D -> kernel -> D2H -> per-packet callback"}

@@ -86,6 +86,13 @@ typedef struct lcb_hash_queue_stats_s {
 	uint64_t	max_gpu_ns;	/* enqueued (or the completer free) -> done. */
 	uint64_t	max_callback_ns; /* a batch's digest copies + callbacks. */
 	uint64_t	max_submit_wait_ns; /* a submit blocked for an open slot. */
+	/* The steps of the launch that set max_launch_ns (ns): reopen (install
+	 * the next open slot), drain (wait for the leases, fill holes), rebase
+	 * (only batches with zero-copy packets: coalesce their runs, rebase
+	 * their addresses), index/length + arena copies enqueued, zero-copy run
+	 * copies enqueued, bucketing + batch kernels enqueued, completion event
+	 * recorded.  Their sum is max_launch_ns. */
+	uint64_t	max_launch_steps_ns[7];
 } lcb_hash_queue_stats_t;
 
 /* Submit flags. */

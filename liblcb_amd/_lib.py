@@ -108,7 +108,8 @@ class QueueStats(ctypes.Structure):
                                      "sealed_flush", "max_batch_msgs", "submit_waits",
                                      "flusher_drain_ns", "flusher_launch_ns", "completer_busy_ns",
                                      "gpu_wait_ns", "max_fill_ns", "max_launch_ns", "max_gpu_ns",
-                                     "max_callback_ns", "max_submit_wait_ns")]
+                                     "max_callback_ns", "max_submit_wait_ns")] + [
+        ("max_launch_steps_ns", c_u64 * 7)]
 
 
 class Seg(ctypes.Structure):

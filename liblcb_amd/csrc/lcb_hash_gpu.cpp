@@ -7,6 +7,7 @@
 // pageable input is gathered into pinned staging by up to 8 host threads.  Every HIP failure maps to an errno code; nothing falls back to the
 // CPU.
 #include <errno.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -531,14 +532,19 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
         uint32_t nseg = 0;
         e = hipMemcpyAsync(&nseg, a.seg, 4, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        std::vector<uint32_t> fl(nseg ? nseg : 1);
+        // (the whole segment region: the flags sit one per 4,352-B block)
+        std::vector<uint32_t> reg((size_t)nseg * kSegBlockWords + 1);
         if (e == hipSuccess && nseg)
-            e = hipMemcpy2DAsync(fl.data(), 4, a.seg + kSegHead + 64 * kSegStateWords, kSegBlockWords * 4, 4, nseg,
-                                 hipMemcpyDeviceToHost, s);
+            e = hipMemcpyAsync(reg.data(), a.seg + kSegHead, (size_t)nseg * kSegBlockWords * 4, hipMemcpyDeviceToHost,
+                               s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         uint32_t h[4] = {nseg, 0, 0, 0};
-        for (uint32_t i = 0; i < nseg && e == hipSuccess; ++i)
-            ++h[fl[i] == kSegTaken ? 1 : fl[i] == (uint32_t)kSegs - 1 ? 2 : 3];
+        for (uint32_t i = 0; i < nseg && e == hipSuccess; ++i) {
+            const uint32_t f = reg[(size_t)i * kSegBlockWords + 64 * kSegStateWords];
+            ++h[f == kSegTaken ? 1 : f == (uint32_t)kSegs - 1 ? 2 : 3];
+            if (f != kSegTaken && f != (uint32_t)kSegs - 1 && h[3] == 1)
+                fprintf(stderr, "lcb seg take-over test: wave %u flag %#x\n", i, f);
+        }
         std::lock_guard<std::mutex> lk(g_seg_mu);
         memcpy(g_seg_last, h, sizeof(h));
     }

@@ -181,12 +181,13 @@ void ensure_peer(int dev, int home) {
 // Pinned result buffers of the device split (device mode), pooled: a
 // hipHostMalloc per call would cost more than the split.
 struct SplitHost {
-    uint64_t* h = nullptr;
+    uint64_t* h = nullptr;          // pinned, coherent: [result words | epoch word]
+    uint32_t epoch = 0;
     bool busy = false;
 };
 std::mutex g_sh_mu;
 std::vector<SplitHost*> g_sh;
-constexpr size_t kSplitWords = 4 * 64 + 1;
+constexpr size_t kSplitWords = 4 * 64 + 2;   // device result block (+ ticket); host: + epoch word
 
 SplitHost* split_host_acquire() {
     std::lock_guard<std::mutex> lk(g_sh_mu);
@@ -196,11 +197,12 @@ SplitHost* split_host_acquire() {
             return x;
         }
     SplitHost* x = new SplitHost();
-    if (hipHostMalloc(reinterpret_cast<void**>(&x->h), kSplitWords * 8, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&x->h), kSplitWords * 8, hipHostMallocCoherent) != hipSuccess) {
         (void)hipGetLastError();
         delete x;
         return nullptr;
     }
+    memset(x->h, 0, kSplitWords * 8);
     x->busy = true;
     g_sh.push_back(x);
     return x;
@@ -260,19 +262,27 @@ int multi_device(const std::vector<Part>& parts, int alg, const uint8_t* key, si
         // Remote part: its byte span [base, end) of the home buffer.
         const uint64_t base = base_of[k], end = end_of[k];
         const uint64_t span = end > base ? end - base : 0;
-        // Slot buffer: [data span | offsets | lengths | digests], 256-B aligned pieces.
+        // Slot buffer: [data span | offsets | lengths | digests], 256-B aligned
+        // pieces.  A copy part on the home device itself (COPY_PARTS) reads
+        // the offsets and lengths where they are: copying them within one
+        // device buys nothing (two enqueues per part less).
+        const bool idx_copy = p.dev != home;
         auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
         const uint64_t o_data = 0, o_off = up(std::max<uint64_t>(span, 1));
-        const uint64_t o_len = o_off + (offsets ? up(n * 8) : 0);
-        const uint64_t o_dig = o_len + (lengths ? up(n * 4) : 0);
+        const uint64_t o_len = o_off + (offsets && idx_copy ? up(n * 8) : 0);
+        const uint64_t o_dig = o_len + (lengths && idx_copy ? up(n * 4) : 0);
         if (fail(slot_reserve(q, o_dig + up(n * D)))) break;
         uint8_t* qd = q->p + o_data;
-        uint64_t* qo = offsets ? reinterpret_cast<uint64_t*>(q->p + o_off) : nullptr;
-        uint32_t* ql = lengths ? reinterpret_cast<uint32_t*>(q->p + o_len) : nullptr;
+        const uint64_t* qo = offsets ? (idx_copy ? reinterpret_cast<uint64_t*>(q->p + o_off) : offsets + p.lo) : nullptr;
+        const uint32_t* ql = lengths ? (idx_copy ? reinterpret_cast<uint32_t*>(q->p + o_len) : lengths + p.lo) : nullptr;
         uint8_t* qg = q->p + o_dig;
         if (span && fail(hipMemcpyPeerAsync(qd, p.dev, data + base, home, span, q->s))) break;
-        if (qo && fail(hipMemcpyPeerAsync(qo, p.dev, offsets + p.lo, home, n * 8, q->s))) break;
-        if (ql && fail(hipMemcpyPeerAsync(ql, p.dev, lengths + p.lo, home, n * 4, q->s))) break;
+        if (qo && idx_copy &&
+            fail(hipMemcpyPeerAsync(const_cast<uint64_t*>(qo), p.dev, offsets + p.lo, home, n * 8, q->s)))
+            break;
+        if (ql && idx_copy &&
+            fail(hipMemcpyPeerAsync(const_cast<uint32_t*>(ql), p.dev, lengths + p.lo, home, n * 4, q->s)))
+            break;
         if (offsets) {
             // message i at (qd - base) + offsets[i]: the copy of the span.
             rc = batch_device(alg, key, key_len, qd - base, qo, ql, n, 0, fixed_len, qg, q->s, nullptr);
@@ -367,16 +377,39 @@ int lcb_hash_batch_multi(const int* devs, int ndev, int alg, const uint8_t* key,
         if (!sh) e = hipErrorOutOfMemory;
         if (e == hipSuccess) e = scratch_alloc(reinterpret_cast<void**>(&dbuf), (nb + kSplitWords) * 8, s);
         if (e == hipSuccess) {
-            launch_multi_split(lengths, offsets, stride, fixed_len, count, (uint32_t)ndev, dbuf, dbuf + nb, s);
+            sh->epoch = (sh->epoch + 1) ? sh->epoch + 1 : 1;
+            launch_multi_split(lengths, offsets, stride, fixed_len, count, (uint32_t)ndev, dbuf, dbuf + nb, sh->h,
+                               sh->epoch, s);
             e = hipGetLastError();
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(sh->h, dbuf + nb, (3 * (size_t)ndev + 1) * 8, hipMemcpyDeviceToHost, s);
             (void)scratch_free(dbuf, s);
         }
     }
     if (e == hipSuccess) e = hipEventRecord(ready, s);
     if (e == hipSuccess && split_dev) {
-        e = hipEventSynchronize(ready);
+        // The split's last block writes the result and then this call's
+        // epoch into the pinned word: spin on it, then poll with short
+        // sleeps; a stream that has drained without it is an error.
+        const uint32_t* flag = reinterpret_cast<const uint32_t*>(sh->h + 4 * 64 + 1);
+        for (uint64_t it = 0;; ++it) {
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == sh->epoch) break;
+            if (it < 20000) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            if ((it & 63) == 0) {
+                const hipError_t q = hipEventQuery(ready);
+                if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != sh->epoch) {
+                    e = hipErrorUnknown;
+                    break;
+                }
+                if (q != hipSuccess && q != hipErrorNotReady) {
+                    e = q;
+                    break;
+                }
+                (void)hipGetLastError();
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(5));
+        }
         if (e == hipSuccess) {
             for (int k = 0; k <= ndev; ++k) first[k] = sh->h[k];
             for (int k = 0; k < ndev; ++k) {

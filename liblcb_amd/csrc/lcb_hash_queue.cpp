@@ -84,6 +84,11 @@ struct alignas(64) LeaseRec {
     // must not clear the announcement of the record's current owner.
     std::atomic<uint32_t> busy{0};
     std::atomic<uint32_t> done{0};   // packets written into this lease
+    // Written by the lease's owner before it publishes `done`: the payload
+    // bytes of its packets and whether one of them is zero-copy, so the
+    // launch sums per lease instead of walking every packet.
+    std::atomic<uint64_t> payload{0};
+    std::atomic<uint32_t> zc{0};
 };
 
 enum SealWhy { kSealFull = 1, kSealTimer = 2, kSealFlush = 3 };
@@ -192,6 +197,7 @@ struct lcb_hash_queue_s {
     std::atomic<uint64_t> max_batch{0}, submit_waits{0};
     std::atomic<uint64_t> drain_ns{0}, launch_ns{0}, completer_ns{0}, gpu_wait_ns{0};
     std::atomic<uint64_t> max_fill{0}, max_launch{0}, max_gpu{0}, max_cb{0}, max_submit_wait{0};
+    std::atomic<uint64_t> max_steps[7] = {};   // the steps of the max_launch batch
     std::atomic<int> first_error{0};
 
     // Zero-copy packet sources (lcb_hash_queue_register): append-only, read
@@ -210,7 +216,7 @@ struct lcb_hash_queue_s {
     void flusher_main();
     void completer_main();
     void drain_leases(Slot* b);
-    void launch(Slot* b, int why);
+    void launch(Slot* b, int why, int64_t* steps);
     void release_all();
     void install_open(Slot* b);      // under m
 };
@@ -234,7 +240,11 @@ bool seal(Slot* b) {
 
 // Reopen a drained slot as a new generation (under m).
 void lcb_hash_queue_s::install_open(Slot* b) {
-    for (size_t r = 0; r < b->nleases; ++r) b->leases[r].done.store(0, std::memory_order_relaxed);
+    for (size_t r = 0; r < b->nleases; ++r) {
+        b->leases[r].done.store(0, std::memory_order_relaxed);
+        b->leases[r].payload.store(0, std::memory_order_relaxed);
+        b->leases[r].zc.store(0, std::memory_order_relaxed);
+    }
     b->t_first.store(0, std::memory_order_relaxed);
     b->closed.store(0, std::memory_order_relaxed);
     b->n = b->bytes = b->payload = b->packets = 0;
@@ -256,78 +266,94 @@ void lcb_hash_queue_s::drain_leases(Slot* b) {
         while (L.busy.load(std::memory_order_seq_cst) != 0) std::this_thread::yield();
         const uint64_t lo = r * lease_msgs + L.done.load(std::memory_order_acquire);
         const uint64_t hi = std::min<uint64_t>(count, (r + 1) * lease_msgs);
+        const uint64_t arena = (uint64_t)reinterpret_cast<uintptr_t>(b->d_data);
         for (uint64_t i = lo; i < hi; ++i) {
-            b->h_off[i] = 0;
+            b->h_off[i] = arena;   // an empty message at the arena's start
             b->h_len[i] = 0;
             b->meta[i] = Meta{nullptr, nullptr, nullptr, 0};
         }
     }
 }
 
-// Enqueue one sealed, drained slot: H2D, kernel, D2H, completion event.
-void lcb_hash_queue_s::launch(Slot* b, int why) {
+// Enqueue one sealed, drained slot: H2D, kernel, completion event.
+// steps[0..4]: ns spent rebasing, enqueueing the index/length/arena copies,
+// the zero-copy run copies, the kernels, the event.
+void lcb_hash_queue_s::launch(Slot* b, int why, int64_t* steps) {
+    int64_t tt[6];
+    tt[0] = now_ns();
     const uint64_t s = b->state.load(std::memory_order_acquire);
     b->n = st_count(s);
     b->bytes = st_bytes(s);
+    // Packets, payload and zero-copy presence from the leases' own sums
+    // (the launch walked every packet -- up to 64K -- on
+    // the flusher's seal-to-launch path).
     size_t payload = 0, packets = 0;
-    // Offsets become absolute device addresses (the batch's `data` is 0):
-    // arena packets at d_data + pos, zero-copy packets where they lie in
-    // host memory (kZeroCopyTag | device address, from the submit).
-    // Zero-copy packets: every producer submits from its own receive buffers
-    // in address order, so a batch's zero-copy packets form a few contiguous
-    // RUNS (one per producer stream; gaps up to kZcGap bytes are bridged).
-    // Runs that lie in one registered region and fit the slot's device arena
-    // beside the copied packets move with one H2D copy each, at the link's
-    // bulk rate, and are hashed from device memory; a packet outside them is
-    // read by the kernel where it lies, over the link.
+    bool any_zc = false;
+    const uint64_t nrec = (b->n + lease_msgs - 1) / lease_msgs;
+    for (uint64_t r = 0; r < nrec; ++r) {
+        const LeaseRec& L = b->leases[r];
+        packets += L.done.load(std::memory_order_acquire);
+        payload += L.payload.load(std::memory_order_relaxed);
+        any_zc |= L.zc.load(std::memory_order_relaxed) != 0;
+    }
+    // Copied packets hold their device address in the arena already (the
+    // producer wrote it); the arena copy covers the bytes the leases
+    // reserved.  Zero-copy packets: every producer submits from its own
+    // receive buffers in address order, so a batch's zero-copy packets form
+    // a few contiguous RUNS (one per producer stream; gaps up to kZcGap
+    // bytes are bridged).  Runs that lie in one registered region and fit
+    // the slot's device arena beside the copied packets move with one H2D
+    // copy each, at the link's bulk rate, and are hashed from device memory;
+    // a packet outside them is read by the kernel where it lies, over the
+    // link.  Only a batch with zero-copy packets walks its packets.
     const uint64_t arena = (uint64_t)reinterpret_cast<uintptr_t>(b->d_data);
     struct Run { uint64_t lo, hi; };
     Run run[kZcRuns];
     int nrun = 0, last = -1;
-    // The arena bytes the copied packets fill (leases reserve room that a
-    // lease's zero-copy packets, or its unused tail, never write).
-    uint64_t aused = 0;
-    for (size_t i = 0; i < b->n; ++i) {
-        const uint64_t o = b->h_off[i];
-        b->zrun[i] = kZcRuns;
-        if (!(o & kZeroCopyTag)) {
-            aused = std::max<uint64_t>(aused, o + b->h_len[i]);
-            continue;
-        }
-        const uint64_t d = o & ~kZeroCopyTag, e = d + b->h_len[i];
-        int r = -1;
-        if (last >= 0 && d >= run[last].hi && d <= run[last].hi + kZcGap) r = last;
-        for (int k = 0; k < nrun && r < 0; ++k)
-            if (d >= run[k].hi && d <= run[k].hi + kZcGap) r = k;
-        if (r < 0 && nrun < kZcRuns) { r = nrun++; run[r].lo = d; run[r].hi = d; }
-        if (r < 0) continue;                       // too many runs: read in place
-        run[r].hi = e;
-        b->zrun[i] = (uint8_t)r;
-        last = r;
-    }
-    // Arena position of each run (after the copied packets, 256-B aligned);
-    // runs that do not fit or leave every registered region stay in place.
+    uint64_t aused = b->bytes;
     uint64_t rpos[kZcRuns];
     const uint8_t* rhost[kZcRuns];
-    uint64_t pos = (aused + 255) & ~255ull;
-    const int nr = nregions.load(std::memory_order_acquire);
-    for (int k = 0; k < nrun; ++k) {
-        rhost[k] = nullptr;
-        const uint64_t len = run[k].hi - run[k].lo;
-        if (pos + len > cfg.max_batch_bytes) continue;
-        for (int g = 0; g < nr && !rhost[k]; ++g)
-            if (run[k].lo >= regions[g].dev && run[k].hi <= regions[g].dev + regions[g].size)
-                rhost[k] = regions[g].host + (run[k].lo - regions[g].dev);
-        if (rhost[k]) { rpos[k] = pos; pos = (pos + len + 255) & ~255ull; }
-    }
-    for (size_t i = 0; i < b->n; ++i) {
-        payload += b->h_len[i];
-        packets += b->meta[i].real;
-        const uint64_t o = b->h_off[i];
-        const int r = b->zrun[i];
-        if (!(o & kZeroCopyTag)) b->h_off[i] = arena + o;
-        else if (r < kZcRuns && rhost[r]) b->h_off[i] = arena + rpos[r] + ((o & ~kZeroCopyTag) - run[r].lo);
-        else b->h_off[i] = o & ~kZeroCopyTag;
+    if (any_zc) {
+        aused = 0;
+        for (size_t i = 0; i < b->n; ++i) {
+            const uint64_t o = b->h_off[i];
+            b->zrun[i] = kZcRuns;
+            if (!(o & kZeroCopyTag)) {
+                aused = std::max<uint64_t>(aused, o - arena + b->h_len[i]);
+                continue;
+            }
+            const uint64_t d = o & ~kZeroCopyTag, e = d + b->h_len[i];
+            int r = -1;
+            if (last >= 0 && d >= run[last].hi && d <= run[last].hi + kZcGap) r = last;
+            for (int k = 0; k < nrun && r < 0; ++k)
+                if (d >= run[k].hi && d <= run[k].hi + kZcGap) r = k;
+            if (r < 0 && nrun < kZcRuns) { r = nrun++; run[r].lo = d; run[r].hi = d; }
+            if (r < 0) continue;                       // too many runs: read in place
+            run[r].hi = e;
+            b->zrun[i] = (uint8_t)r;
+            last = r;
+        }
+        // Arena position of each run (after the copied packets, 256-B
+        // aligned); runs that do not fit or leave every registered region
+        // stay in place.
+        uint64_t pos = (aused + 255) & ~255ull;
+        const int nr = nregions.load(std::memory_order_acquire);
+        for (int k = 0; k < nrun; ++k) {
+            rhost[k] = nullptr;
+            const uint64_t len = run[k].hi - run[k].lo;
+            if (pos + len > cfg.max_batch_bytes) continue;
+            for (int g = 0; g < nr && !rhost[k]; ++g)
+                if (run[k].lo >= regions[g].dev && run[k].hi <= regions[g].dev + regions[g].size)
+                    rhost[k] = regions[g].host + (run[k].lo - regions[g].dev);
+            if (rhost[k]) { rpos[k] = pos; pos = (pos + len + 255) & ~255ull; }
+        }
+        for (size_t i = 0; i < b->n; ++i) {
+            const uint64_t o = b->h_off[i];
+            if (!(o & kZeroCopyTag)) continue;
+            const int r = b->zrun[i];
+            if (r < kZcRuns && rhost[r]) b->h_off[i] = arena + rpos[r] + ((o & ~kZeroCopyTag) - run[r].lo);
+            else b->h_off[i] = o & ~kZeroCopyTag;
+        }
     }
     b->payload = payload;
     b->packets = packets;
@@ -340,33 +366,29 @@ void lcb_hash_queue_s::launch(Slot* b, int why) {
     // -- the p99 half-load tail of BENCH_r04 -- LCB_QUEUE_TRACE)
     a.count = b->n; a.stride = 0; a.fixed_len = 0; a.digests = b->h_dig; a.mid = mid;
     int rc = 0;
-    // LCB_QUEUE_TRACE=1: report any launch step over 1 ms on stderr
-    // (diagnostics of the zero-copy latency tail).
-    static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
-    int64_t tt[8];
-    int nt = 0;
-    tt[nt++] = now_ns();
+    tt[1] = now_ns();
     if (hipMemcpyAsync(b->d_off, b->h_off, b->n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b->d_len, b->h_len, b->n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
         (aused && hipMemcpyAsync(b->d_data, b->h_data, aused, hipMemcpyHostToDevice, st) != hipSuccess))
         rc = EIO;
-    tt[nt++] = now_ns();
+    tt[2] = now_ns();
     for (int k = 0; k < nrun && !rc; ++k)
         if (rhost[k] && run[k].hi > run[k].lo &&
             hipMemcpyAsync(b->d_data + rpos[k], rhost[k], run[k].hi - run[k].lo, hipMemcpyHostToDevice, st) != hipSuccess)
             rc = EIO;
-    tt[nt++] = now_ns();
+    tt[3] = now_ns();
     if (!rc) rc = launch_ordered(alg, a, st, b->d_work);
-    tt[nt++] = now_ns();
-    tt[nt++] = now_ns();
+    tt[4] = now_ns();
     if (!rc && hipEventRecord(b->done, st) != hipSuccess) rc = EIO;
-    tt[nt++] = now_ns();
-    if (trace && tt[nt - 1] - tt[0] > 1000000)
-        fprintf(stderr, "lcb_hash_queue: slow launch seq=%llu n=%zu runs=%d aused=%llu: idx/len %.0f us, runs %.0f us, "
-                "kernel %.0f us, -- %.0f us, event %.0f us\n", (unsigned long long)b->seq, b->n, nrun,
-                (unsigned long long)aused,
-                (tt[1] - tt[0]) * 1e-3, (tt[2] - tt[1]) * 1e-3, (tt[3] - tt[2]) * 1e-3, (tt[4] - tt[3]) * 1e-3,
-                (tt[5] - tt[4]) * 1e-3);
+    tt[5] = now_ns();
+    for (int k = 0; k < 5; ++k) steps[k] = tt[k + 1] - tt[k];
+    // LCB_QUEUE_TRACE=1: report any launch over 1 ms on stderr as well.
+    static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+    if (trace && tt[5] - tt[0] > 1000000)
+        fprintf(stderr, "lcb_hash_queue: slow launch seq=%llu n=%zu runs=%d aused=%llu: rebase %.0f us, "
+                "idx/len %.0f us, runs %.0f us, kernel %.0f us, event %.0f us\n", (unsigned long long)b->seq, b->n,
+                nrun, (unsigned long long)aused, steps[0] * 1e-3, steps[1] * 1e-3, steps[2] * 1e-3, steps[3] * 1e-3,
+                steps[4] * 1e-3);
     b->launch_err = rc;
     b->t_launch = now_ns();
     batches.fetch_add(1, std::memory_order_relaxed);
@@ -444,9 +466,14 @@ void lcb_hash_queue_s::flusher_main() {
             fprintf(stderr, "lcb_hash_queue: slow seal -> launch: reopen %.0f us, drain %.0f us\n",
                     (t_busy - b->t_seal) * 1e-3, (t_launch - t_busy) * 1e-3);
         const int64_t t_seal = b->t_seal;
-        launch(b, why);   // b may complete and be reused from here on: no access
+        int64_t steps[7] = {t_busy - t_seal, t_launch - t_busy, 0, 0, 0, 0, 0};
+        launch(b, why, steps + 2);   // b may complete and be reused from here on: no access
         const int64_t t_end = now_ns();
-        note_max(max_launch, t_end - t_seal);
+        if (t_end - t_seal > (int64_t)max_launch.load(std::memory_order_relaxed)) {
+            // (the flusher is the only writer)
+            for (int k = 0; k < 7; ++k) max_steps[k].store((uint64_t)steps[k], std::memory_order_relaxed);
+            max_launch.store((uint64_t)(t_end - t_seal), std::memory_order_relaxed);
+        }
         drain_ns.fetch_add(t_launch - t_busy, std::memory_order_relaxed);
         launch_ns.fetch_add(t_end - t_launch, std::memory_order_relaxed);
         if (!reopened) {
@@ -651,19 +678,30 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
         }
     }
     if (!rc) {
-        // One empty message through the batch path: the process's first
-        // kernel launch loads the library's code object (4-5 ms, LCB_QUEUE_TRACE),
-        // which would otherwise land on the first batch's packets.
+        // Empty messages through the batch paths a batch takes: the first
+        // launch of a kernel loads its code object (4-5 ms for the first,
+        // LCB_QUEUE_TRACE), which would otherwise land on the first batches'
+        // packets -- one message (the per-lane kernel), then a bucketed
+        // batch (the bucketing and tile kernels: their first launch on a
+        // full batch held the flusher 0.9 ms, BENCH r7b max_launch_steps_us
+        // "kernels", and the packets of that batch made the p999).
         Slot& b = q->slots[0];
-        KArgs a;
-        a.data = nullptr; a.offsets = b.d_off; a.lengths = b.d_len; a.order = nullptr;
-        a.count = 1; a.stride = 0; a.fixed_len = 0; a.digests = b.h_dig; a.mid = q->mid;
-        *reinterpret_cast<uint64_t*>(b.h_off) = (uint64_t)reinterpret_cast<uintptr_t>(b.d_data);
-        b.h_len[0] = 0;
-        if (hipMemcpyAsync(b.d_off, b.h_off, 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
-            hipMemcpyAsync(b.d_len, b.h_len, 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
-            launch_ordered(alg, a, b.stream, b.d_work) != 0 || hipStreamSynchronize(b.stream) != hipSuccess)
-            rc = EIO;
+        const uint64_t warm[2] = {1, std::min<uint64_t>(cfg.max_batch_msgs, kBucketMinCount)};
+        for (int w = 0; w < 2 && !rc; ++w) {
+            const uint64_t n = warm[w];
+            if (w == 1 && n < kBucketMinCount) break;
+            for (uint64_t i = 0; i < n; ++i) {
+                b.h_off[i] = (uint64_t)reinterpret_cast<uintptr_t>(b.d_data);
+                b.h_len[i] = 0;
+            }
+            KArgs a;
+            a.data = nullptr; a.offsets = b.d_off; a.lengths = b.d_len; a.order = nullptr;
+            a.count = n; a.stride = 0; a.fixed_len = 0; a.digests = b.h_dig; a.mid = q->mid;
+            if (hipMemcpyAsync(b.d_off, b.h_off, n * 8, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+                hipMemcpyAsync(b.d_len, b.h_len, n * 4, hipMemcpyHostToDevice, b.stream) != hipSuccess ||
+                launch_ordered(alg, a, b.stream, b.d_work) != 0 || hipStreamSynchronize(b.stream) != hipSuccess)
+                rc = EIO;
+        }
     }
     if (rc) {
         q->release_all();
@@ -729,9 +767,13 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
                     _mm_sfence();  // streaming stores before the release of `done`
                 }
                 const uint64_t i = L.idx;
-                b->h_off[i] = zc ? zc : pos;
+                // copied packets: their device address in the arena already
+                // (no rebase pass at launch)
+                b->h_off[i] = zc ? zc : (uint64_t)reinterpret_cast<uintptr_t>(b->d_data) + pos;
                 b->h_len[i] = (uint32_t)len;
                 b->meta[i] = Meta{digest, cb, udata, 1};
+                r.payload.store(r.payload.load(std::memory_order_relaxed) + len, std::memory_order_relaxed);
+                if (zc) r.zc.store(1, std::memory_order_relaxed);
                 L.idx = i + 1;
                 L.pos = pos + clen;
                 r.done.store((uint32_t)(L.idx - (uint64_t)L.rec * LM), std::memory_order_release);
@@ -881,6 +923,7 @@ int lcb_hash_queue_stats(lcb_hash_queue_p q, lcb_hash_queue_stats_t* st) {
     st->max_gpu_ns = q->max_gpu.load();
     st->max_callback_ns = q->max_cb.load();
     st->max_submit_wait_ns = q->max_submit_wait.load();
+    for (int k = 0; k < 7; ++k) st->max_launch_steps_ns[k] = q->max_steps[k].load();
     return 0;
 }
 

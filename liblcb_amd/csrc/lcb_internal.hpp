@@ -251,11 +251,14 @@ void launch_probe(int mode, const KArgs& a, uint32_t* sink, hipStream_t s);
 void launch_gost_lps_probe(uint64_t count, uint32_t fixed_len, uint32_t* sink, hipStream_t s);
 // lcb_hash_batch_multi device mode: the work-balanced split of a batch of
 // `count` messages into nparts (<= 64) and each part's byte span, on `s`:
-// res = [first 0..n | base 0..n-1 | end 0..n-1 | targets] (4 n + 1 words),
-// bsum: split_blocks(count) words.
+// res (device, 4 x 64 + 2 words) = [first 0..n | base 0..n-1 | end 0..n-1 |
+// targets ... | ticket], bsum: (count + split_chunk - 1) / split_chunk
+// words.  The first 3 n + 1 words land in hres (pinned, coherent host
+// memory), then hres word 4 x 64 + 1 (as uint32) = epoch.
 uint64_t split_chunk(uint64_t count);
 void launch_multi_split(const uint32_t* lengths, const uint64_t* offsets, uint64_t stride, uint32_t fixed_len,
-                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, hipStream_t s);
+                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, uint64_t* hres,
+                        uint32_t epoch, hipStream_t s);
 // lcb_hash_gpu_clock_stamp: `slots` one-wave workgroups, 3 uint64 each.
 void launch_clock_stamp(uint64_t* out, uint32_t slots, hipStream_t s);
 void gost_table_host(uint64_t* out);

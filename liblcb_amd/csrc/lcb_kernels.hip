@@ -619,12 +619,14 @@ __global__ __launch_bounds__(kSplitThreads) void split_scan_kernel(uint64_t* bsu
     if (t >= 1 && t < n) {   // T_t = floor(W t / n), exactly: (W / n) t + (W % n) t / n
         r[3 * n + t] = (W / n) * t + (W % n) * t / n;
     }
+    if (t == 0) r[4 * 64 + 1] = 0;   // the place kernel's ticket
 }
 
 __global__ __launch_bounds__(kSplitThreads) void split_place_kernel(const uint32_t* lengths, const uint64_t* offsets,
                                                                     uint64_t stride, uint32_t fixed_len,
                                                                     uint64_t count, uint64_t chunk,
-                                                                    const uint64_t* bbase, uint32_t n, uint64_t* res) {
+                                                                    const uint64_t* bbase, uint32_t n, uint64_t* res,
+                                                                    uint32_t* ticket, uint64_t* hres, uint32_t epoch) {
     __shared__ uint64_t tg[64];         // targets T_1..T_{n-1} (ragged) or first[0..n] (equal work)
     __shared__ unsigned long long lmin[64], lmax[64];
     __shared__ uint64_t wsum[kSplitThreads / 64];
@@ -692,6 +694,28 @@ __global__ __launch_bounds__(kSplitThreads) void split_place_kernel(const uint32
         atomicMin(reinterpret_cast<unsigned long long*>(gptr(r) + n + 1 + t), lmin[t]);
         atomicMax(reinterpret_cast<unsigned long long*>(gptr(r) + 2 * n + 1 + t), lmax[t]);
     }
+    // The last block to finish hands the result to the host's pinned,
+    // coherent buffer (system-scope stores, then the call's epoch released
+    // after them): the host polls one word instead of a copy command and
+    // an event (host time per call).
+    __shared__ uint32_t last_s;
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        last_s = __hip_atomic_fetch_add(gptr(ticket), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    __threadfence();
+    if (t <= 3 * n)
+        __hip_atomic_store(hres + t, __hip_atomic_load(gptr(r) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (t == 0) {
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(hres + 4 * 64 + 1), epoch, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 uint64_t split_chunk(uint64_t count) {
@@ -701,14 +725,15 @@ uint64_t split_chunk(uint64_t count) {
 }
 
 void launch_multi_split(const uint32_t* lengths, const uint64_t* offsets, uint64_t stride, uint32_t fixed_len,
-                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, hipStream_t s) {
+                        uint64_t count, uint32_t nparts, uint64_t* bsum, uint64_t* res, uint64_t* hres,
+                        uint32_t epoch, hipStream_t s) {
     const uint64_t chunk = split_chunk(count);
     const uint32_t nb = (uint32_t)((count + chunk - 1) / chunk);
     hipLaunchKernelGGL(split_sum_kernel, dim3(nb), dim3(kSplitThreads), 0, s, lengths, fixed_len, count, chunk, bsum);
     hipLaunchKernelGGL(split_scan_kernel, dim3(1), dim3(kSplitThreads), 0, s, bsum, nb, count, nparts,
                        lengths != nullptr, res);
     hipLaunchKernelGGL(split_place_kernel, dim3(nb), dim3(kSplitThreads), 0, s, lengths, offsets, stride, fixed_len,
-                       count, chunk, bsum, nparts, res);
+                       count, chunk, bsum, nparts, res, reinterpret_cast<uint32_t*>(res + 4 * 64 + 1), hres, epoch);
 }
 
 }  // namespace lcbgpu

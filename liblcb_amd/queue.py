@@ -142,7 +142,9 @@ class HashQueue:
     def stats(self):
         st = QueueStats()
         check(lib().lcb_hash_queue_stats(self._q, ctypes.byref(st)))
-        return {n: int(getattr(st, n)) for n, _ in QueueStats._fields_}
+        def val(v):
+            return [int(x) for x in v] if isinstance(v, ctypes.Array) else int(v)
+        return {n: val(getattr(st, n)) for n, _ in QueueStats._fields_}
 
     def close(self):
         if self._q:

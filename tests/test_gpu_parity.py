@@ -593,12 +593,19 @@ def test_segmented_takeover(gpu, alg, monkeypatch):
     batch with segmenting off, and the flags read back
     (lcb_hash_gpu_seg_last) show the waves taken over."""
     import ctypes
+    # lengths within 7/8 of each other (61,440..65,536 B), so a tile's
+    # whole-block lines are most of it and it is cut (md_tiles.hpp)
     tiles = 2726 if alg in (2, 3, 4) else 5456
     n = tiles * 64
     rng = np.random.default_rng(160 + alg)
-    lens = rng.integers(32704, 40001, n).astype(np.uint32)
+    lens = rng.integers(61440, 65537, n).astype(np.uint32)
     offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 16, n - 1).astype(np.uint64))
+    # SHA-384/512 (md_lines_kernel) stream only 16-B aligned records
+    gap = rng.integers(0, 16, n - 1).astype(np.uint64)
+    step = lens[:-1].astype(np.uint64) + gap
+    if alg in (5, 6):
+        step = (step + 15) // 16 * 16
+    offs[1:] = np.cumsum(step)
     total = int(offs[-1] + lens[-1]) + 64
     data = gpu.gen_synthetic(0x7A6 + alg, total)
     do = torch.as_tensor(offs.astype(np.int64), device="cuda")

@@ -238,7 +238,9 @@ int main(int argc, char** argv) {
            "\"lat_us_max\": %.1f, \"batches\": %llu, \"sealed_full\": %llu, \"sealed_timer\": %llu, "
            "\"sealed_flush\": %llu, \"submit_waits\": %llu, \"cb\": %d, \"drain_ms\": %.2f, \"launch_ms\": %.2f, "
            "\"completer_busy_ms\": %.2f, \"gpu_wait_ms\": %.2f, \"max_fill_us\": %.1f, \"max_launch_us\": %.1f, "
-           "\"max_gpu_us\": %.1f, \"max_callback_us\": %.1f, \"max_submit_wait_us\": %.1f}\n",
+           "\"max_gpu_us\": %.1f, \"max_callback_us\": %.1f, \"max_submit_wait_us\": %.1f, "
+           "\"max_launch_steps_us\": {\"reopen\": %.1f, \"drain\": %.1f, \"rebase\": %.1f, \"copies\": %.1f, "
+           "\"runs\": %.1f, \"kernels\": %.1f, \"event\": %.1f}}\n",
            alg, (int)zerocopy, rate, lat[packets * 999 / 1000], lat2[lat2.size() * 99 / 100], lat2.back(), (double)worst / packets,
            (unsigned long long)packets, (unsigned long long)size, threads, cfg.flush_usec,
            (unsigned long long)cfg.max_batch_msgs, (unsigned long long)cfg.max_batch_bytes, cfg.batches, (unsigned long long)pool_mib, sec,
@@ -250,7 +252,10 @@ int main(int argc, char** argv) {
            (unsigned long long)(st.submit_waits - st0.submit_waits), (int)use_cb,
            (st.flusher_drain_ns - st0.flusher_drain_ns) * 1e-6, (st.flusher_launch_ns - st0.flusher_launch_ns) * 1e-6, (st.completer_busy_ns - st0.completer_busy_ns) * 1e-6,
            (st.gpu_wait_ns - st0.gpu_wait_ns) * 1e-6, st.max_fill_ns * 1e-3, st.max_launch_ns * 1e-3,
-           st.max_gpu_ns * 1e-3, st.max_callback_ns * 1e-3, st.max_submit_wait_ns * 1e-3);
+           st.max_gpu_ns * 1e-3, st.max_callback_ns * 1e-3, st.max_submit_wait_ns * 1e-3,
+           st.max_launch_steps_ns[0] * 1e-3, st.max_launch_steps_ns[1] * 1e-3, st.max_launch_steps_ns[2] * 1e-3,
+           st.max_launch_steps_ns[3] * 1e-3, st.max_launch_steps_ns[4] * 1e-3, st.max_launch_steps_ns[5] * 1e-3,
+           st.max_launch_steps_ns[6] * 1e-3);
     if (!out.empty()) {
         FILE* f = fopen(out.c_str(), "wb");
         if (!f || fwrite(digests.data(), 1, digests.size(), f) != digests.size()) return 1;
