@@ -20,7 +20,8 @@ OUT = os.path.join(ROOT, "tests", "golden", "codesize.json")
 def measure(so=SO):
     kr = runpy.run_path(os.path.join(ROOT, "tools", "kernel_resources.py"))
     cos = kr["code_objects"](so)
-    names = sorted(set(r["name"] for r in kr["kernels"](so)))
+    # kernel names with their template arguments, without the parameter list
+    names = sorted(set(r["name"].split("(")[0] for r in kr["kernels"](so)))
     return {"so_bytes": os.path.getsize(so), "code_object_bytes": sum(len(c) for c in cos),
             "kernels": names}
 
