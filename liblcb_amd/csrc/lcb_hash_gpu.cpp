@@ -187,8 +187,10 @@ StreamScratch* stream_scratch_acquire(hipStream_t s, size_t bytes) {
             e->p = nullptr;
             return nullptr;
         }
-        // Header zeroed in stream order: flag 0 (epochs start at 1), counter 0.
-        if (hipMemsetAsync(e->p, 0, kStreamScratchHeader, s) != hipSuccess) {
+        // Header zeroed in stream order: flag 0 (epochs start at 1), counter
+        // 0; and the bucketing head of the payload (the one-kernel
+        // bucketing's sync words start at zero and stay so between uses).
+        if (hipMemsetAsync(e->p, 0, kStreamScratchHeader + kBucketWork * sizeof(uint32_t), s) != hipSuccess) {
             (void)hipGetLastError();
             (void)hipFree(e->p);
             e->p = nullptr;
@@ -513,6 +515,8 @@ int launch_ordered(int alg, KArgs a, hipStream_t s, uint32_t* work_buf) {
         } else {
             LCB_TRY(scratch_alloc(reinterpret_cast<void**>(&work), bytes, s));
             pooled = true;
+            // a pool block: the bucketing's sync words must start at zero
+            LCB_TRY(hipMemsetAsync(work + kBucketSync, 0, kBucketSyncWords * sizeof(uint32_t), s));
         }
         const bool tiles = tiles_take(alg, a);
         const uint32_t seg_min = cap ? tile_slots(alg) : 0u;

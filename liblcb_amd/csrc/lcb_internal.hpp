@@ -90,7 +90,15 @@ constexpr int kBucketKeys = kBucketClasses * kBucketPhases;
 // message.
 constexpr int kBucketHead = 2 * kBucketKeys;
 constexpr int kBucketNTiles = 2 * kBucketKeys + 1;   // entries of `order`, pads included
-constexpr int kBucketWork = 2 * kBucketKeys + 2;
+// The one-kernel bucketing's synchronisation words (bucket_fused_kernel):
+// zero between uses (its last block resets them; a fresh scratch buffer is
+// zeroed once), then `order`.
+constexpr int kBucketSync = 2 * kBucketKeys + 2;
+constexpr int kBucketSyncWords = 64;
+constexpr int kBucketWork = 2 * kBucketKeys + 2 + kBucketSyncWords;
+// Groups of chunks of the one-kernel bucketing (at most kBucketGroupsMax):
+// the last chunk counted in a group scans the group's counts.
+constexpr uint32_t kBucketGroupsMax = 56;
 // Messages per bucketing block: count / 1024, clamped to [4096, 8192] (the
 // placement sorts a block's whole chunk in LDS).
 constexpr uint64_t kBucketBlocksTarget = 1024;
@@ -156,7 +164,7 @@ inline size_t bucket_seg_words(uint32_t seg_cap) {
 }
 inline size_t bucket_seg_offset(uint64_t count) {
     const size_t w = (size_t)kBucketWork + bucket_order_words(count) + 2 * bucket_blocks(count) * kBucketKeys +
-                     (count + 1) / 2;
+                     (count + 1) / 2 + (size_t)kBucketGroupsMax * kBucketKeys;   // ... group sums
     return (w + 63) / 64 * 64;
 }
 inline size_t bucket_words(uint64_t count, uint32_t seg_cap = 0) {

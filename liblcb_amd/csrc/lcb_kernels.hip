@@ -2,6 +2,9 @@
 // per algorithm: k_<alg>.hip, gost_kernels.hip) and the shared utility
 // kernels: synthetic input, HBM read probes, length bucketing.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <algorithm>
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
 
@@ -410,6 +413,286 @@ __global__ __launch_bounds__(1024) void bucket_place_kernel(KArgs a, uint64_t ch
     for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
 }
 
+// ------------------------------------------------ one-kernel bucketing
+// The same counting sort as one kernel (the three
+// kernels above spend 24.5 us per packet pass, most of it three kernels'
+// fixed start and end costs).  Its blocks take work by TICKET, not by
+// blockIdx: tickets 0..nb-1 count chunk t, tickets nb..2nb-1 place chunk
+// t - nb.  A placing block waits for every chunk's count, and every count
+// ticket was drawn before any place ticket, i.e. by a block that is
+// running (counting never waits): no grid size or co-residency can
+// deadlock it.  Chunks form `ng` groups of G; the block that counts a
+// group's last chunk scans the group's counts (per key: the exclusive
+// prefix over the group's chunks, and the group total), so what is serial
+// after the last count is one group's scan; each placing block adds the
+// group totals itself (ng x 488 words), recomputes its messages' keys
+// (12 B of offset + length each, rather than a key array written by one
+// block and read by another) and then places as bucket_place_kernel.
+// Cross-block words (counts, prefixes, group totals) move as agent-scope
+// atomic stores and loads, each writer waiting for its stores (vmcnt)
+// before it bumps a counter -- no release / acquire fences, which write
+// back and invalidate a whole XCD's L2 each (a first form with them ran the
+// packet pass 120 us slower).  The sync words (kBucketSync: ticket, groups
+// done, one counter per group) are zero at entry; the block that draws the
+// last ticket of all resets them.
+struct BucketSync {
+    uint32_t* w;
+    __device__ uint32_t* ticket() const { return w; }
+    __device__ uint32_t* groups_done() const { return w + 1; }
+    __device__ uint32_t* group(uint32_t g) const { return w + 8 + g; }
+};
+static_assert(8 + kBucketGroupsMax <= (uint32_t)kBucketSyncWords, "sync words");
+
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(gptr(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool kTiles, bool kCheck>
+__global__ __launch_bounds__(1024) void bucket_fused_kernel(KArgs a, uint64_t chunk, uint32_t nb, uint32_t G,
+                                                            uint32_t ng, uint32_t* cnt, uint32_t* inb, uint32_t* gsum,
+                                                            uint32_t* work, uint32_t* order, uint32_t seg_min,
+                                                            uint32_t seg_simds, uint32_t* seg_flags, uint32_t seg_cap,
+                                                            uint32_t seg_test) {
+    __shared__ uint32_t h[kBucketKeys];        // count: histogram; place: run start of this chunk's entries
+    __shared__ uint32_t loc[kBucketKeys];      // place: local (sorted) offset per key, then the fill cursor
+    __shared__ uint32_t len_s[kBucketKeys];
+    __shared__ uint32_t sidx[kBucketChunkMax];
+    __shared__ uint16_t skey[kBucketChunkMax];
+    __shared__ uint32_t misc[4];
+    const uint32_t t = threadIdx.x;
+    const BucketSync sy{gptr(work) + kBucketSync};
+    constexpr int kPer = (kBucketKeys + 63) / 64;
+    for (;;) {
+        if (t == 0) misc[2] = __hip_atomic_fetch_add(sy.ticket(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t tk = misc[2];
+        __syncthreads();
+        if (tk >= 2 * nb) {
+            // Every block draws exactly one ticket past the work; the one
+            // that draws the last leaves the sync words zero for the next use
+            // (no other block touches them any more).
+            if (tk == 2 * nb + gridDim.x - 1 && t < (uint32_t)kBucketSyncWords) st_agent(sy.w + t, 0u);
+            return;
+        }
+        const uint32_t c = tk < nb ? tk : tk - nb;
+        const uint64_t lo = (uint64_t)c * chunk;
+        const uint64_t hi = lo + chunk < a.count ? lo + chunk : a.count;
+        const uint32_t g = c / G;
+        if (tk < nb) {
+            // ------------------------------------------------ count chunk c
+            for (uint32_t k = t; k < (uint32_t)kBucketKeys; k += blockDim.x) h[k] = 0;
+            __syncthreads();
+            bool bad = false;
+            for (uint64_t i0 = lo + t; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
+                uint32_t k[kBucketUnroll], ki[kBucketUnroll];
+#pragma unroll
+                for (int u = 0; u < kBucketUnroll; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                    k[u] = i < hi ? bucket_key(a, i) : 0u;
+                    if constexpr (kCheck) ki[u] = i < hi ? gptr(a.key_index)[i] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kBucketUnroll; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                    if (i < hi) {
+                        atomicAdd(&h[k[u]], 1u);
+                        if constexpr (kCheck) bad |= ki[u] >= a.nkeys;
+                    }
+                }
+            }
+            if constexpr (kCheck) {
+                bad = __syncthreads_or(bad);
+                if (bad && t == 0) st_agent(const_cast<uint32_t*>(a.bad), a.bad_epoch);
+            } else {
+                __syncthreads();
+            }
+            for (uint32_t k = t; k < (uint32_t)kBucketKeys; k += blockDim.x)
+                st_agent(cnt + (uint64_t)c * kBucketKeys + k, h[k]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's stores done
+            __syncthreads();                                    // ... and every thread's
+            const uint32_t gsz = (g + 1) * G <= nb ? G : nb - g * G;
+            if (t == 0)
+                misc[3] = __hip_atomic_fetch_add(sy.group(g), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gsz;
+            __syncthreads();
+            if (!misc[3]) continue;
+            // The group's last chunk: per key, the exclusive prefix over the
+            // group's chunks (inb) and the group total (gsum).
+            if (t < (uint32_t)kBucketKeys) {
+                uint32_t v[16];
+                uint32_t run = 0;
+                for (uint32_t j0 = 0; j0 < gsz; j0 += 16) {   // 16 loads in flight per thread
+#pragma unroll
+                    for (int u = 0; u < 16; ++u)
+                        v[u] = j0 + u < gsz ? ld_agent(cnt + (uint64_t)(g * G + j0 + u) * kBucketKeys + t) : 0u;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        if (j0 + u < gsz) st_agent(inb + (uint64_t)(g * G + j0 + u) * kBucketKeys + t, run);
+                        run += v[u];
+                    }
+                }
+                st_agent(gsum + (uint64_t)g * kBucketKeys + t, run);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) {
+                const uint32_t done = __hip_atomic_fetch_add(sy.groups_done(), 1u, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT) + 1;
+                if (kCheck && done == ng && a.check_host) {
+                    // every chunk counted: the fused key-index check is final
+                    const uint32_t bv = ld_agent(a.bad);
+                    __hip_atomic_store(a.check_host, a.bad_epoch | (bv == a.bad_epoch ? 0x80000000u : 0u),
+                                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+            continue;
+        }
+        // ------------------------------------------------ place chunk c
+        // This chunk's first keys do not depend on the other chunks: their
+        // loads go out before the wait.  (A safety valve, never reached by a
+        // well-formed launch: after 1 s -- 10^8 ticks of the 100 MHz clock
+        // -- the block gives its chunk up rather than spin for ever, so a
+        // corrupted sync word cannot hang the GPU; the last block still
+        // resets the words.)
+        uint32_t k0[kBucketUnroll];
+#pragma unroll
+        for (int u = 0; u < kBucketUnroll; ++u) {
+            const uint64_t i = lo + t + (uint64_t)u * blockDim.x;
+            k0[u] = i < hi ? bucket_key(a, i) : 0u;
+        }
+        if (t == 0) {
+            misc[3] = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t spins = 0;
+            while (ld_agent(sy.groups_done()) < ng) {
+                if (++spins > 4) __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                    misc[3] = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (misc[3]) {
+            __syncthreads();
+            continue;
+        }
+        // Per key: this chunk's count, the total (all groups) and this
+        // chunk's base (the groups before its own, plus its prefix inside it).
+        // (16 loads in flight per thread: the group totals are ng rows)
+        uint32_t hk = 0, bk = 0, ck = 0;
+        if (t < (uint32_t)kBucketKeys) {
+            ck = ld_agent(cnt + (uint64_t)c * kBucketKeys + t);
+            bk = ld_agent(inb + (uint64_t)c * kBucketKeys + t);
+            for (uint32_t q0 = 0; q0 < ng; q0 += 16) {
+                uint32_t v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = q0 + u < ng ? ld_agent(gsum + (uint64_t)(q0 + u) * kBucketKeys + t) : 0u;
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    hk += v[u];
+                    bk += q0 + u < g ? v[u] : 0u;
+                }
+            }
+        }
+        // (from here as bucket_place_kernel, chunk c)
+        const int used = __syncthreads_count(hk != 0);
+        const bool pad = kTiles && a.count >= kBucketPadRatio * 64 * (uint64_t)used;
+        if (t < (uint32_t)kBucketKeys) {
+            len_s[t] = pad ? (hk + 63u) & ~63u : hk;
+            loc[t] = ck;     // this chunk's counts (scanned below)
+        }
+        __syncthreads();
+        if (t < 64) {
+            uint32_t v[kPer], sm = 0;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int k = kBucketKeys - 1 - (kPer * (int)t + u);
+                v[u] = k >= 0 ? len_s[k] : 0u;
+                sm += v[u];
+            }
+            const uint32_t incl = wave_scan_incl(sm, t);
+            uint32_t e = incl - sm;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int k = kBucketKeys - 1 - (kPer * (int)t + u);
+                if (k >= 0) h[k] = e;
+                e += v[u];
+            }
+            if (t == 63) misc[0] = incl;
+        } else if (t < 128) {
+            const uint32_t l = t - 64;
+            uint32_t cv[kPer], sm = 0;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int k = kPer * (int)l + u;
+                cv[u] = k < kBucketKeys ? loc[k] : 0u;
+                sm += cv[u];
+            }
+            uint32_t e = wave_scan_incl(sm, l) - sm;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int k = kPer * (int)l + u;
+                if (k < kBucketKeys) loc[k] = e;
+                e += cv[u];
+            }
+        }
+        __syncthreads();
+        constexpr uint32_t kSegKey = kSegMinClass * kBucketPhases;
+        if (t < (uint32_t)kBucketKeys) {
+            const uint32_t start = h[t];
+            if (c == 0)
+                for (uint32_t e = start + hk; e < start + len_s[t]; ++e) gptr(order)[e] = kOrderPad;
+            if (t == kSegKey - 1) {
+                const uint64_t n = (start + 63) / 64, sm = seg_simds ? seg_simds : 1;
+                const uint64_t a0 = (n + sm - 1) / sm * sm, a3 = (kSegs * n + sm - 1) / sm * sm;
+                const bool pays = 100 * kSegs * a0 > 103 * a3 && 4 * n >= 5 * (uint64_t)seg_min;
+                misc[1] = (seg_min && seg_simds && pays && n <= seg_cap) ? (uint32_t)n : 0u;
+            }
+            h[t] = start + bk - loc[t];
+        }
+        if (c == 0 && t == 0) gptr(work)[kBucketNTiles] = misc[0];
+        __syncthreads();
+        if (seg_min) {
+            const uint32_t nseg = misc[1];
+            for (uint32_t i = c * blockDim.x + t; i < nseg; i += nb * blockDim.x)
+                gptr(seg_flags)[kSegHead + (uint64_t)i * kSegBlockWords + 64 * kSegStateWords] = 0u;
+            if (c == 0 && t < 4) {
+                const uint32_t hv[4] = {nseg, seg_test ? 1u : 0u, 0u, seg_test ? 1u : 0u};
+                gptr(seg_flags)[t] = hv[t];
+            }
+        }
+        for (uint64_t i0 = lo + t; i0 < hi; i0 += kBucketUnroll * blockDim.x) {
+            uint32_t k[kBucketUnroll];
+            if (i0 == lo + t) {
+#pragma unroll
+                for (int u = 0; u < kBucketUnroll; ++u) k[u] = k0[u];
+            } else {
+#pragma unroll
+                for (int u = 0; u < kBucketUnroll; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                    k[u] = i < hi ? bucket_key(a, i) : 0u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kBucketUnroll; ++u) {
+                const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                if (i < hi) {
+                    const uint32_t p = atomicAdd(&loc[k[u]], 1u);
+                    sidx[p] = (uint32_t)i;
+                    skey[p] = (uint16_t)k[u];
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t n = (uint32_t)(hi - lo);
+        for (uint32_t p = t; p < n; p += blockDim.x) gptr(order)[h[skey[p]] + p] = sidx[p];
+        __syncthreads();
+    }
+}
+
 void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tiles, uint32_t seg_min, bool seg_test,
                       hipStream_t s) {
     // work: [tot | spare | spare | entry count] then `order`
@@ -421,6 +704,37 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tile
     uint32_t* cnt = order + bucket_order_words(a.count);
     uint32_t* base = cnt + (uint64_t)nb * kBucketKeys;
     uint16_t* keys = reinterpret_cast<uint16_t*>(base + (uint64_t)nb * kBucketKeys);
+    // LCB_BUCKET_FUSED=1 in the environment: the one-kernel form.  Not the
+    // default: same-process A/Bs with rocprofv3 kernel traces measured it at
+    // 26.3 us median per 1M-packet bucketing against 25.1 for the three
+    // kernels (profiles/r7_bucket_fused_ab.txt) -- the serial
+    // chain inside one kernel (count, a group's scan, the wait, the place)
+    // costs what the two kernel boundaries cost.
+    const char* fe = getenv("LCB_BUCKET_FUSED");
+    if (fe && fe[0] == '1') {
+        uint32_t* gsum = reinterpret_cast<uint32_t*>(keys) + (a.count + 1) / 2;
+        uint32_t G = 1;
+        while (G * G < nb) ++G;                                            // ~sqrt(nb) chunks per group
+        if ((nb + G - 1) / G > kBucketGroupsMax) G = (nb + kBucketGroupsMax - 1) / kBucketGroupsMax;
+        const uint32_t ng = (nb + G - 1) / G;
+        const uint32_t simds = 4u * (uint32_t)device_cu_count();
+        // one block per CU (97 VGPRs x 16 waves: one 1,024-thread block fits a
+        // CU): each block then counts a chunk and places one, and only the
+        // grid's own blocks draw the exit tickets (a grid of 2 nb dispatched
+        // a second round of blocks just to exit)
+        const uint32_t grid = std::min<uint32_t>(nb, (uint32_t)device_cu_count());
+        const uint32_t sm = a.seg ? seg_min : 0u, st = seg_test ? 1u : 0u;
+#define LCB_FUSED(T, C)                                                                                      \
+    hipLaunchKernelGGL((bucket_fused_kernel<T, C>), dim3(grid), dim3(1024), 0, s, a, chunk, nb, G, ng, cnt, base, \
+                       gsum, work, order, sm, simds, a.seg, a.seg_cap, st)
+        if (tiles) {
+            if (a.check_host) LCB_FUSED(true, true); else LCB_FUSED(true, false);
+        } else {
+            if (a.check_host) LCB_FUSED(false, true); else LCB_FUSED(false, false);
+        }
+#undef LCB_FUSED
+        return;
+    }
     if (a.check_host)
         hipLaunchKernelGGL(bucket_count_kernel<true>, dim3(nb), dim3(1024), 0, s, a, chunk, nb, cnt, keys);
     else

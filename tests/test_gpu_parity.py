@@ -630,6 +630,35 @@ def test_segmented_takeover(gpu, alg, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alg", [1, 6])
+def test_bucketing_one_kernel_form(gpu, alg, monkeypatch):
+    """The one-kernel bucketing (LCB_BUCKET_FUSED=1, lcb_kernels.hip
+    bucket_fused_kernel: ticket-ordered count and place phases) gives the
+    same digests as the default three-kernel form: the 1M-packet layout
+    (tile kernel, padded runs; MD5) and a 300K-message mix with segmented
+    long waves (SHA-512, unpadded), three passes each (its sync words reset
+    between uses), and a keyed batch (the fused key-index check)."""
+    from tests.golden_util import packet_layout
+    offs, lens, total = packet_layout()
+    data = gpu.gen_synthetic(0xB0C, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    ref = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    monkeypatch.setenv("LCB_BUCKET_FUSED", "1")
+    for rep in range(3):
+        got = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+        assert np.array_equal(got, ref), (alg, rep)
+    kidx = torch.as_tensor((np.arange(len(lens)) % 5).astype(np.int32), device="cuda")
+    keys = [bytes([k]) * (7 * k + 1) for k in range(5)]
+    kf = gpu.hash_batch_keyed(alg, 1, keys, data, key_index=kidx, offsets=do, lengths=dl).cpu().numpy()
+    monkeypatch.delenv("LCB_BUCKET_FUSED")
+    kr = gpu.hash_batch_keyed(alg, 1, keys, data, key_index=kidx, offsets=do, lengths=dl).cpu().numpy()
+    assert np.array_equal(kf, kr), alg
+    del data
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
 def test_bucketing_large_chunks(gpu, oracle):
     """ragged batches above 4M messages bucket in chunks of
     4097..8192 messages (two unrolled steps per thread, ~1,000 blocks), a
