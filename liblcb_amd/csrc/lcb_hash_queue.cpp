@@ -505,6 +505,12 @@ void lcb_hash_queue_s::completer_main() {
         const int64_t t_cb = now_ns();
         gpu_wait_ns.fetch_add(t_cb - t_wait, std::memory_order_relaxed);
         note_max(max_gpu, t_cb - std::max(t_wait, b->t_launch));
+        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+        if (trace && t_cb - std::max(t_wait, b->t_launch) > 1000000)
+            fprintf(stderr, "lcb_hash_queue: slow batch seq=%llu n=%zu bytes=%zu packets=%zu: launched %.0f us after "
+                    "its seal, done %.0f us after launch (completer free %.0f us after launch)\n",
+                    (unsigned long long)b->seq, b->n, b->bytes, b->packets, (b->t_launch - b->t_seal) * 1e-3,
+                    (t_cb - b->t_launch) * 1e-3, (t_wait - b->t_launch) * 1e-3);
         for (size_t i = 0; i < b->n; ++i) {
             const Meta& mt = b->meta[i];
             if (!mt.real) continue;

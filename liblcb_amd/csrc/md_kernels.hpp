@@ -139,6 +139,11 @@ struct TileTrace {
 #ifndef LCB_FIXED_PERSIST
 #define LCB_FIXED_PERSIST 4
 #endif
+// SHA-1 on the resident grid too (A/B builds only, tools/build_variant.sh
+// -DLCB_PERSIST_SHA1=1).
+#ifndef LCB_PERSIST_SHA1
+#define LCB_PERSIST_SHA1 0
+#endif
 #ifndef LCB_FIXED_PPRIO
 #define LCB_FIXED_PPRIO 1
 #endif
@@ -585,7 +590,8 @@ void launch_md(const KArgs& a, bool hmac, hipStream_t s) {
         if (fixed_stride_lines(a)) {
             constexpr unsigned T = 64 * kFixedWaves;
             const dim3 grid((unsigned)((a.count + T - 1) / T));
-            if constexpr (kFixedPersist > 0 && std::is_same<H, Md5>::value) {
+            if constexpr (kFixedPersist > 0 && (std::is_same<H, Md5>::value ||
+                                                (LCB_PERSIST_SHA1 && std::is_same<H, Sha1>::value))) {
                 const uint64_t cap = (uint64_t)kFixedPersist * device_cu_count();
                 if (grid.x > cap && cap % 8 == 0) {
                     const dim3 pg((unsigned)cap);

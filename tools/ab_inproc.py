@@ -33,7 +33,7 @@ CRC_IDS = {n: v for v, n in CRC_NAMES.items()}
 
 def load(name):
     path = os.path.join(ROOT, "liblcb_amd", "liblcb_hash_gpu.so") if name == "product" else \
-        os.path.join(ROOT, "build_exp", name, "liblcb_hash_gpu.so")
+        os.path.join(ROOT, "ab_builds", name, "liblcb_hash_gpu.so")
     L = ctypes.CDLL(path)
     for fn, res, args in SIGNATURES + CRC_SIGNATURES:
         if hasattr(L, fn):

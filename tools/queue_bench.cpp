@@ -182,11 +182,21 @@ int main(int argc, char** argv) {
     lcb_hash_queue_stats(q, &st0);
 
     std::atomic<int> fail{0};
-    const int64_t t0 = now_ns();
+    // The producers are started first and released together: t0 is taken
+    // when every one of them is running (round 5 took it before spawning
+    // them, so the last producer's first packets were already late by the
+    // threads' start-up -- charged to the queue as latency: worst_at 0.875,
+    // the 8th producer's first packet, in every run).
+    std::atomic<int> ready{0}, go{0};
+    std::atomic<int64_t> t0a{0};
+    int64_t t0 = 0;
     {
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t)
             th.emplace_back([&, t] {
+                ready.fetch_add(1);
+                while (!go.load(std::memory_order_acquire)) _mm_pause();
+                const int64_t t0 = t0a.load(std::memory_order_relaxed);
                 if (rate > 0) {
                     // contiguous packets per producer (as without --rate); the
                     // k-th packet of producer t is due at (k * threads + t) / rate
@@ -210,6 +220,10 @@ int main(int argc, char** argv) {
                     if (r) { fail.store(r); return; }
                 }
             });
+        while (ready.load() < threads) _mm_pause();
+        t0 = now_ns();
+        t0a.store(t0, std::memory_order_relaxed);
+        go.store(1, std::memory_order_release);
         for (auto& x : th) x.join();
     }
     rc = lcb_hash_queue_wait(q);
