@@ -80,6 +80,8 @@ def parse(argv=None):
     p.add_argument("--no-extras", action="store_true", help="skip per_alg / e2e")
     p.add_argument("--no-gather", action="store_true", help="skip the RCCL digest gather + fixture check")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--settle", default="gen", choices=("self", "gen"),
+                   help="headline warm-up: the synthetic-stream generator (default) or the measured kernel itself")
     p.add_argument("--plan", action="store_true",
                    help="print every rank's shard (gloo, no GPU use) and exit: launch-path check")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -144,18 +146,27 @@ def max_over_ranks(t, world):
     return float(tt.item())
 
 
-def settle(seconds=0.4):
-    """Bring the GPU to its sustained-load clock/power state before a timed
-    segment, with a DIFFERENT kernel (the synthetic-stream generator writing
-    a 256 MiB scratch buffer) so rocprofv3's per-kernel statistics of the
-    measured kernels only contain steady-state launches.  Measured on MI355X:
-    the first ~100 launches of a cold 0.2 ms kernel swing 205-292 us while
-    the power manager reacts (profiles/r1b_bench_kernel_trace.csv)."""
-    scratch = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+def settle(seconds=0.4, launch=None):
+    """Bring the GPU to a loaded clock/power state before a timed segment:
+    `seconds` of back-to-back `launch()` calls, by default the
+    synthetic-stream generator writing a 256 MiB scratch buffer (so
+    rocprofv3's per-kernel statistics of the measured kernels only hold
+    steady-state launches).  Measured on MI355X: the first ~100 launches of
+    a cold 0.2 ms kernel swing 205-292 us while the power manager reacts
+    (profiles/r1b_bench_kernel_trace.csv).  `--settle self` warms up with the
+    measured kernel instead: in fresh processes alternating on one box the
+    two gave the same headline (5,185 vs 5,188 GiB/s over three pairs, the
+    in-run clock 1.80-1.99 GHz either way; profiles/r7_settle_ab.txt)."""
+    scratch = None
+    if launch is None:
+        scratch = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+
+        def launch():
+            liblcb_amd.gen_synthetic(1, scratch.numel(), out=scratch)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for _ in range(20):
-            liblcb_amd.gen_synthetic(1, scratch.numel(), out=scratch)
+            launch()
         torch.cuda.synchronize()
     del scratch
 
@@ -908,7 +919,8 @@ def main():
     digests = torch.empty((max(count, 1), D), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
 
-    settle()
+    sp = torch.cuda.current_stream().cuda_stream
+    settle(launch=(lambda: check(hash_launch(alg, data, digests, count, sp))) if a.settle == "self" else None)
     t, kms, clock = time_alg(alg, data, digests, count, a.steps, a.warmup, world)
     value = total * MSG_LEN * a.steps / t / 2**30
     alg_bytes = count * (MSG_LEN + D)      # read every message once + write its digest
