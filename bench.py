@@ -237,12 +237,43 @@ class ClockWindow:
         return out
 
 
-def valu_frac_at(vfloor_ms, clock, kms):
-    """The VALU issue floor (valu_floor_ms: at 2.4 GHz) at the clock the
-    timed launches ran at, over their kernel time."""
+def valu_frac_at(vfloor_ms, clock, kms, cpi=None):
+    """The VALU issue floor (valu_floor_ms: 4 cycles per instruction at
+    2.4 GHz) at the clock the timed launches ran at, over their kernel time;
+    with `cpi` (valu_cpi) the floor at the kernel's own measured cycles per
+    VALU instruction instead of the 4-cycle model."""
     if not vfloor_ms or not clock or not clock.get("clock_GHz"):
         return None
-    return round(vfloor_ms * (VALU_CLOCK_HZ / 1e9) / clock["clock_GHz"] / kms, 4)
+    f = vfloor_ms * (VALU_CLOCK_HZ / 1e9) / clock["clock_GHz"] / kms
+    if cpi:
+        f *= cpi / VALU_CYCLES
+    return round(f, 4)
+
+
+# The kernel each algorithm's occupancy pass measured (sha224 / sha384 /
+# gost512 run the same body as their siblings).
+_OCC_SIBLING = {"sha224": "sha256", "sha384": "sha512", "gost512": "gost256"}
+
+
+def valu_cpi(alg):
+    """Cycles per VALU instruction of this algorithm's kernel: 4 (the
+    mixed-stream model of DESIGN.md 5), or fewer when the PMC occupancy pass
+    (profiles/valu_counts.json: SQ_ACTIVE_INST_VALU x 4 over the same pass's
+    SQ_BUSY_CYCLES, one run, its own clock) saw the kernel issue faster than
+    that -- its mix holds full-rate operations (v_xor / v_bitop3 / v_add_u32
+    at 2.2-2.6 cycles alone, profiles/r1_valu_rate.txt): MD5 3.73, GOST 3.82,
+    SHA-512 3.91, SHA-256 3.94, SHA-1 4.00 (r7p).  The floor can then not read
+    above 1 merely because the model is 4 cycles."""
+    name = ALG_NAMES[alg]
+    try:
+        algs = json.load(open(os.path.join(ROOT, "profiles", "valu_counts.json")))["algs"]
+        rec = algs[_OCC_SIBLING.get(name, name)]
+        if not counters_current(rec):
+            return None
+        u = float(rec["occupancy"]["valu_issue_util_median"])
+    except (OSError, ValueError, KeyError):
+        return None
+    return round(VALU_CYCLES / max(1.0, u), 3)
 
 
 def hash_launch(alg, data, digests, count, stream, key=None):
@@ -342,28 +373,15 @@ def valu_floor_ms(alg, count):
     return n * VALU_CYCLES / (VALU_SIMDS * VALU_CLOCK_HZ) * 1e3
 
 
-def pmc_clock_ghz(alg):
-    """Median engine clock the PMC occupancy pass measured under this
-    algorithm's kernel (profiles/valu_counts.json `occupancy`, SQ_CYCLES per
-    engine / dispatch time), None when absent or stale."""
-    try:
-        rec = json.load(open(os.path.join(ROOT, "profiles", "valu_counts.json")))["algs"][ALG_NAMES[alg]]
-        if not counters_current(rec):
-            return None
-        return float(rec["occupancy"]["clock_GHz_median"])
-    except (OSError, ValueError, KeyError):
-        return None
-
-
 LDS_BYTES_PER_CLK_CU = 256   # ds_read_b64 array rate per CU (MI355X_MICROARCH.md LDS)
 N_CUS = 256
 
 
-def gost_lds_array(name, count, kernel_ms):
+def gost_lds_array(name, count, kernel_ms, clock=None):
     """GOST against the LDS array's peak: the table
     gathers' bytes -- 1 KiB message = 17 g_N + 2 g_0 = 19 g x 25 LPS, each 64
     ds_read_b64 of 8 B: 475 x 512 B -- over the kernel time, as a fraction of
-    256 B/clk/CU x 256 CUs at 2.4 GHz and at the PMC-measured clock, plus the
+    256 B/clk/CU x 256 CUs at 2.4 GHz and at the timed launches' clock, plus the
     bank-conflict share of the LDS-array cycles from the committed counters
     (profiles/pmc_gost_lds.json, when its code stamp matches)."""
     lps = (MSG_LEN // 64 + 1 + 2) * 25
@@ -376,9 +394,9 @@ def gost_lds_array(name, count, kernel_ms):
             out["lds_bank_conflict_share"] = rec["bank_conflict_share"]
     except (OSError, ValueError, KeyError):
         pass
-    clk = pmc_clock_ghz(ALG_IDS[name])
-    if clk:
-        out["lds_array_frac_pmc_clock"] = round(gbytes / (kernel_ms * 1e-3) / (LDS_BYTES_PER_CLK_CU * N_CUS * clk * 1e9), 4)
+    clk = clock.get("clock_GHz") if clock else None
+    if clk:   # at the clock of the timed launches themselves
+        out["lds_array_frac_run_clock"] = round(gbytes / (kernel_ms * 1e-3) / (LDS_BYTES_PER_CLK_CU * N_CUS * clk * 1e9), 4)
     return out
 
 
@@ -961,18 +979,16 @@ def main():
                      # engine clock of the timed launches (rank 0's), and the
                      # VALU floor at that clock
                      "clock": clock,
-                     "valu_frac_run_clock": valu_frac_at(vfloor, clock, kms)},
+                     "valu_frac_run_clock_4c": valu_frac_at(vfloor, clock, kms),
+                     "valu_cpi": valu_cpi(alg),
+                     "valu_frac_run_clock": valu_frac_at(vfloor, clock, kms, valu_cpi(alg))},
     }
     from liblcb_amd._lib import LIB_PATH
     out["library_sha256_16"] = hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()[:16]
-    clk = pmc_clock_ghz(alg)
-    if vfloor and clk:
-        # The same VALU floor at the clock the kernel actually runs at (the
-        # 2.4 GHz of valu_floor_ms is the spec maximum; the power manager
-        # holds MD5 near 2.1).
-        f = vfloor * VALU_CLOCK_HZ / (clk * 1e9)
-        out["roofline"].update({"pmc_clock_GHz": clk, "valu_floor_ms_pmc_clock": round(f, 4),
-                                "valu_frac_pmc_clock": round(f / kms, 4)})
+    # (Round 5 scaled the floor by the clock of the separate PMC pass
+    # instead, valu_frac_pmc_clock: a different run's clock, which put three
+    # of them above 1 -- VERDICT r5.  The floor is now taken at the clock of
+    # the timed launches themselves, `clock` above.)
 
     if rank == 0 and world == 1 and not a.no_extras:
         # Achievable read rate on this box next to the spec peak: the same
@@ -1009,13 +1025,9 @@ def main():
                          "kernel_ms": round(km, 4),
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "valu_frac": round(vf / km, 4) if vf else None,
-                         "clock": ck, "valu_frac_run_clock": valu_frac_at(vf, ck, km)}
-            clk = pmc_clock_ghz(aid)
-            if vf and clk:
-                # The same floor at the clock the PMC pass measured under this
-                # kernel (the power manager's, not the spec 2.4 GHz).
-                per[name]["pmc_clock_GHz"] = clk
-                per[name]["valu_frac_pmc_clock"] = round(vf * (VALU_CLOCK_HZ / 1e9 / clk) / km, 4)
+                         "clock": ck, "valu_cpi": valu_cpi(aid),
+                         "valu_frac_run_clock_4c": valu_frac_at(vf, ck, km),
+                         "valu_frac_run_clock": valu_frac_at(vf, ck, km, valu_cpi(aid))}
             if name.startswith("gost"):
                 # GOST is bound by its LDS table gathers, not HBM or VALU:
                 # the gathers alone, same grid and image, beside the kernel.
@@ -1025,7 +1037,7 @@ def main():
                     lps_ms = per["gost256"]["lps_chain_ms"]
                 per[name]["lps_chain_ms"] = round(lps_ms, 4)
                 per[name]["lds_frac"] = round(lps_ms / km, 4)
-                per[name].update(gost_lds_array(name, count, km))
+                per[name].update(gost_lds_array(name, count, km, ck))
             del dg
         out["per_alg"] = per
         # Batched HMAC (RADIUS needs HMAC-MD5): per call
