@@ -606,7 +606,7 @@ def gather_digests(digests, first, n, total, world, rank):
     return torch.cat(out).cpu().numpy(), ms
 
 
-def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
+def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU, key=None):
     """BASELINE configs[3]: 1M buffers, lengths {64 B, 1 KiB, 64 KiB} chosen by
     mix64(seed + i) % 3, packed, device resident.  The library
     buckets the ragged batch by length on the device (counted in the time).
@@ -614,7 +614,9 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
     headline; MD5, SHA-1 and SHA-224/256 run the tile kernel, SHA-384/512 the
     LDS line stream and GOST the per-lane kernel over the bucketed order),
     each checked against
-    the reference's digest-of-digests."""
+    the reference's digest-of-digests.  With `key`: HMAC rows (named
+    hmac_<alg>), checked against the same batch with segmented waves off
+    (LCB_TILE_SEGS=0), which no reference fixture covers."""
     from tests.golden_util import mixed_lengths
     lens = np.array(mixed_lengths(SEED, count), dtype=np.uint32)
     offs = np.zeros(count, dtype=np.uint64)
@@ -636,8 +638,8 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
         dig = torch.empty((count, D), dtype=torch.uint8, device="cuda")
 
         def launch():
-            check(lib().lcb_hash_batch(alg, None, 0, data.data_ptr(), do.data_ptr(), dl.data_ptr(), count,
-                                       0, 0, dig.data_ptr(), F_DEVICE, stream.cuda_stream))
+            check(lib().lcb_hash_batch(alg, key, len(key) if key else 0, data.data_ptr(), do.data_ptr(),
+                                       dl.data_ptr(), count, 0, 0, dig.data_ptr(), F_DEVICE, stream.cuda_stream))
         n = steps if alg == algs[0] else 3
         for _ in range(warmup if alg == algs[0] else 1):
             launch()
@@ -655,10 +657,17 @@ def bench_c4(algs, warmup, steps, count=MSGS_PER_GPU):
                "hbm_frac": round(ab / t / 1e9 / HBM_PEAK_GBS, 4),
                "clock": cw.result(t * n * 1e3),
                "lengths": "{64, 1024, 65536}[mix64(seed+i) % 3]", "bucketed": True}
-        if ref is not None:
+        if key is not None:
+            got = dig.cpu().numpy().tobytes()
+            os.environ["LCB_TILE_SEGS"] = "0"
+            launch()
+            torch.cuda.synchronize()
+            os.environ.pop("LCB_TILE_SEGS", None)
+            res["digests_equal_unsegmented"] = got == dig.cpu().numpy().tobytes()
+        elif ref is not None:
             res["dod_equals_reference"] = hashlib.sha256(dig.cpu().numpy().tobytes()).hexdigest() == \
                 ref["algs"][ALG_NAMES[alg]]["dod"]
-        out[ALG_NAMES[alg]] = res
+        out[("hmac_" if key is not None else "") + ALG_NAMES[alg]] = res
         del dig
     del data
     torch.cuda.empty_cache()
@@ -1075,6 +1084,19 @@ def main():
                     r["fixed_stride_ratio_per_block"] = round(
                         r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
                         blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+        # HMAC-MD5 on C4 (segmented long waves through the
+        # HMAC tile kernel's one copy), its per-compression ratio to the
+        # fixed-stride HMAC-MD5 row above (HMAC: one outer compression more
+        # per message).
+        c4h = bench_c4([ALG_IDS["md5"]], 1, 3, key=key)["hmac_md5"]
+
+        def hmac_blocks_per_byte(lens):
+            return float((((lens + 1 + 8 + 63) // 64) + 1).sum() * 64) / float(lens.sum())
+        c4h["fixed_stride_GiB_s"] = hm["hmac_md5"]["GiB_s"]
+        c4h["fixed_stride_ratio_per_block"] = round(
+            c4h["GiB_s"] / hm["hmac_md5"]["GiB_s"] * hmac_blocks_per_byte(c4_lens) /
+            hmac_blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+        c4["hmac_md5"] = c4h
         out["ragged_c4_per_alg"] = c4
         out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4),
                                               ref_clock=clock["clock_GHz"] if clock else None)

@@ -466,8 +466,9 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const
 
 // Segmented long waves of a bucketed batch: the wave capacity its scratch
 // holds (0: this batch is never segmented).  The tile kernel's plain MD5 /
-// SHA-1 / SHA-256 digests (md_tiles.hpp: segmented copies cost code size)
-// and md_lines_kernel (SHA-384/512, plain and HMAC) take segmented waves;
+// SHA-1 / SHA-256 digests and HMAC-MD5 (md_tiles.hpp: segmented copies cost
+// code size) and md_lines_kernel (SHA-384/512, plain and HMAC) take
+// segmented waves;
 // batches of other modes get no state region (every ragged
 // batch paid 64 B per message for it).  LCB_TILE_SEGS=0 in the environment
 // turns segmenting off (read per call: the tests compare both forms in one
@@ -475,7 +476,8 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const
 static uint32_t seg_capacity(int alg, const KArgs& a) {
     if (!a.lengths || a.order != nullptr || a.count < kBucketMinCount || a.count >= kBucketMaxCount) return 0;
     const bool tiles = tiles_take(alg, a);
-    const bool seg_kernel = tiles ? a.key_mode == kKeyNone && a.mid == nullptr && (alg == 1 || alg == 2 || alg == 4)
+    const bool seg_kernel = tiles ? a.key_mode == kKeyNone && ((a.mid == nullptr && (alg == 1 || alg == 2 || alg == 4)) ||
+                                                               (a.mid != nullptr && alg == 1))
                                   : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
     if (!seg_kernel) return 0;
     const char* ev = getenv("LCB_TILE_SEGS");

@@ -773,7 +773,13 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // mode (33 MB) ran its first 20 timed fixed-stride steps 7 % slower than
     // one without (18 MB), the same kernel, fresh processes alternating
     // (profiles/r6_codesize_headline.txt).
-    constexpr bool kSegMode = kMode == kTilePlain && !std::is_same<H, Sha256<true>>::value;
+    // HMAC-MD5 takes segmented jobs through ONE copy
+    // of its line loop, the segmented one, for segmented and whole tiles
+    // alike: no second copy, so no code growth (the packet tiles pay the
+    // segment paths' registers: one copy with both paths ran the plain
+    // packets 0.5 % slower, below).
+    constexpr bool kSegHmac = kMode == kTileHmac && std::is_same<H, Md5>::value;
+    constexpr bool kSegMode = (kMode == kTilePlain && !std::is_same<H, Sha256<true>>::value) || kSegHmac;
     const bool uniform = __all(Rl == R);
     if (js.nsegs > 1 && (!kSegMode || !uniform)) {
         // a segmented tile that cannot be cut: segment 0 runs it whole (one
@@ -782,7 +788,7 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
         js.nsegs = 1;
     }
     if (uniform) {
-        if constexpr (kSegMode && LCB_TILE_ONECOPY) {
+        if constexpr (kSegMode && (LCB_TILE_ONECOPY || kSegHmac)) {
             md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));
         } else if constexpr (kSegMode) {
             if (js.nsegs > 1) md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));

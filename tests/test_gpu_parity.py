@@ -582,8 +582,8 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alg", [1, 2, 4, 6])
-def test_segmented_takeover(gpu, alg, monkeypatch):
+@pytest.mark.parametrize("alg,key", [(1, None), (1, b"seg-hmac-key"), (2, None), (4, None), (6, None)])
+def test_segmented_takeover(gpu, alg, key, monkeypatch):
     """the take-over path of segmented jobs (seg_jobs.hpp
     seg_wait): with LCB_SEG_TAKEOVER=1 the jobs of every cut wave run in
     reverse segment order with no wait, so each wave's last segment starts
@@ -611,10 +611,10 @@ def test_segmented_takeover(gpu, alg, monkeypatch):
     do = torch.as_tensor(offs.astype(np.int64), device="cuda")
     dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
     monkeypatch.setenv("LCB_TILE_SEGS", "0")
-    whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
     monkeypatch.delenv("LCB_TILE_SEGS")
     monkeypatch.setenv("LCB_SEG_TAKEOVER", "1")
-    taken = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    taken = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
     st = (ctypes.c_uint32 * 4)()
     assert gpu.lib().lcb_hash_gpu_seg_last(st) == 0
     monkeypatch.delenv("LCB_SEG_TAKEOVER")
@@ -623,8 +623,19 @@ def test_segmented_takeover(gpu, alg, monkeypatch):
     assert np.array_equal(taken, whole), alg
     assert nseg > 0 and ntaken >= 0.9 * nseg and inorder == 0, list(st)
     # and the normal order again (the knob is per call)
-    again = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    again = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
     assert np.array_equal(again, whole), alg
+    if key is not None:   # HMAC-MD5's segmented tiles against the oracle, sampled
+        from oracle.pyoracle import Oracle
+        pick = np.sort(rng.choice(n, 64, replace=False))
+        parts, soff, pos = [], np.zeros(len(pick), np.uint64), 0
+        for j, i in enumerate(pick):
+            o, ln = int(offs[i]), int(lens[i])
+            parts.append(data[o:o + ln].cpu().numpy())
+            soff[j] = pos
+            pos += ln
+        exp = Oracle().batch(alg, np.concatenate(parts), soff, lens[pick], key=key)
+        assert np.array_equal(again[pick], exp)
     del data
     torch.cuda.empty_cache()
 
