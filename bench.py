@@ -1084,6 +1084,12 @@ def main():
                     r["fixed_stride_ratio_per_block"] = round(
                         r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
                         blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+                    # the same at equal engine clocks (both passes' in-run
+                    # clocks: VALU-bound kernels scale with it)
+                    if r.get("clock") and per[name].get("clock"):
+                        r["fixed_stride_ratio_per_block_equal_clock"] = round(
+                            r["fixed_stride_ratio_per_block"] * per[name]["clock"]["clock_GHz"] /
+                            r["clock"]["clock_GHz"], 3)
         # HMAC-MD5 on C4 (segmented long waves through the
         # HMAC tile kernel's one copy), its per-compression ratio to the
         # fixed-stride HMAC-MD5 row above (HMAC: one outer compression more
@@ -1096,6 +1102,9 @@ def main():
         c4h["fixed_stride_ratio_per_block"] = round(
             c4h["GiB_s"] / hm["hmac_md5"]["GiB_s"] * hmac_blocks_per_byte(c4_lens) /
             hmac_blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+        if c4h.get("clock") and hm["hmac_md5"].get("clock_GHz"):
+            c4h["fixed_stride_ratio_per_block_equal_clock"] = round(
+                c4h["fixed_stride_ratio_per_block"] * hm["hmac_md5"]["clock_GHz"] / c4h["clock"]["clock_GHz"], 3)
         c4["hmac_md5"] = c4h
         out["ragged_c4_per_alg"] = c4
         out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4),
