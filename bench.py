@@ -833,6 +833,21 @@ def bench_chacha(data, count, steps):
     return res
 
 
+def _cgroup_throttle():
+    """(throttled periods, throttled us) of this process's cgroup CPU quota,
+    or None where no cpu.stat is readable (cgroup v2, then v1)."""
+    for f, scale in (("/sys/fs/cgroup/cpu.stat", 1.0), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-3),
+                     ("/sys/fs/cgroup/cpu,cpuacct/cpu.stat", 1e-3)):
+        try:
+            kv = dict(ln.split()[:2] for ln in open(f) if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        us = kv.get("throttled_usec")
+        us = float(us) if us is not None else float(kv.get("throttled_time", 0)) * scale
+        return int(kv.get("nr_throttled", 0)), us
+    return None
+
+
 def bench_ingest(alg_id, packets=1 << 21, threads=8):
     """Asynchronous ingestion queue (include/lcb_hash_queue.h, SURVEY.md 8f
     row 2): `threads` native producer threads submit 1 KiB packets from host
@@ -849,10 +864,23 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
             "--threads", str(threads)]
 
     def run(extra):
-        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
+        # LCB_QUEUE_TRACE=1: the queue logs every stall over 1 ms (a slow
+        # launch step, a batch picked up late by the completion thread, the
+        # flusher waiting for a free slot, a submit waiting for an open
+        # slot) with its time in the run; the host's CPU throttling (cgroup
+        # cpu.stat) is read around the run, so a stall caused by the box's
+        # CPU quota shows as such in the record.
+        env = dict(os.environ, LCB_QUEUE_TRACE="1")
+        t0 = _cgroup_throttle()
+        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300, env=env)
+        t1 = _cgroup_throttle()
         if r.returncode != 0:
             raise RuntimeError(r.stderr.strip()[-300:])
-        return json.loads(r.stdout.strip().splitlines()[-1])
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        out["stall_trace"] = [ln.strip() for ln in r.stderr.splitlines() if "lcb_hash_queue:" in ln][:8]
+        out["cgroup_throttled"] = None if t0 is None or t1 is None else \
+            {"periods": t1[0] - t0[0], "us": round(t1[1] - t0[1], 1)}
+        return out
     try:
         sat = run([])
         half = run(["--rate", str(int(sat["packets_per_s"] / 2))])
@@ -869,7 +897,7 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
         # The slowest launch's own steps ride along.
         return {k: r.get(k) for k in ("max_fill_us", "max_launch_us", "max_launch_steps_us", "max_gpu_us",
                                       "max_callback_us", "max_submit_wait_us", "submit_waits", "worst_at",
-                                      "lat_us_max", "late_half_p99")}
+                                      "lat_us_max", "late_half_p99", "stall_trace", "cgroup_throttled")}
     return {"packets_per_s": sat["packets_per_s"], "GiB_s": sat["GiB_s"], "batches": sat["batches"],
             # Zero-copy submit (LCB_HASH_Q_F_ZEROCOPY): packets already in a
             # registered page-locked pool (the io_buf receive buffers,

@@ -195,6 +195,7 @@ struct lcb_hash_queue_s {
     std::atomic<uint64_t> completed{0}, completed_bytes{0};
     std::atomic<uint64_t> batches{0}, sealed_full{0}, sealed_timer{0}, sealed_flush{0};
     std::atomic<uint64_t> max_batch{0}, submit_waits{0};
+    const int64_t t_create = now_ns();   // trace timestamps are relative to it
     std::atomic<uint64_t> drain_ns{0}, launch_ns{0}, completer_ns{0}, gpu_wait_ns{0};
     std::atomic<uint64_t> max_fill{0}, max_launch{0}, max_gpu{0}, max_cb{0}, max_submit_wait{0};
     std::atomic<uint64_t> max_steps[7] = {};   // the steps of the max_launch batch
@@ -477,20 +478,27 @@ void lcb_hash_queue_s::flusher_main() {
         drain_ns.fetch_add(t_launch - t_busy, std::memory_order_relaxed);
         launch_ns.fetch_add(t_end - t_launch, std::memory_order_relaxed);
         if (!reopened) {
+            const int64_t t_fw = now_ns();
+            size_t nin = 0;
             {
                 std::unique_lock<std::mutex> lk(m);
+                nin = inflight.size();
                 cv_free.wait(lk, [&] { return !free_slots.empty(); });
                 Slot* next = free_slots.front();
                 free_slots.pop_front();
                 install_open(next);
             }
             cv_open.notify_all();
+            if (trace && now_ns() - t_fw > 1000000)
+                fprintf(stderr, "lcb_hash_queue: t=%.0f us flusher waited %.0f us for a free slot (%zu in flight)\n",
+                        (t_fw - t_create) * 1e-3, (now_ns() - t_fw) * 1e-3, nin);
         }
     }
 }
 
 void lcb_hash_queue_s::completer_main() {
     (void)hipSetDevice(device);
+    int64_t prev_end = 0;
     for (;;) {
         Slot* b = nullptr;
         {
@@ -500,12 +508,16 @@ void lcb_hash_queue_s::completer_main() {
             b = inflight.front();
         }
         const int64_t t_wait = now_ns();
+        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+        if (trace && t_wait - std::max(prev_end, b->t_launch) > 1000000)
+            fprintf(stderr, "lcb_hash_queue: t=%.0f us completer took batch seq=%llu up %.0f us late\n",
+                    (t_wait - t_create) * 1e-3, (unsigned long long)b->seq,
+                    (t_wait - std::max(prev_end, b->t_launch)) * 1e-3);
         int err = b->launch_err;
         if (!err) err = map_err(hipEventSynchronize(b->done));
         const int64_t t_cb = now_ns();
         gpu_wait_ns.fetch_add(t_cb - t_wait, std::memory_order_relaxed);
         note_max(max_gpu, t_cb - std::max(t_wait, b->t_launch));
-        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
         if (trace && t_cb - std::max(t_wait, b->t_launch) > 1000000)
             fprintf(stderr, "lcb_hash_queue: slow batch seq=%llu n=%zu bytes=%zu packets=%zu: launched %.0f us after "
                     "its seal, done %.0f us after launch (completer free %.0f us after launch)\n",
@@ -535,6 +547,7 @@ void lcb_hash_queue_s::completer_main() {
         }
         cv_free.notify_one();
         cv_done.notify_all();
+        prev_end = now_ns();
     }
 }
 
@@ -849,7 +862,12 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
         if (q->open.load(std::memory_order_acquire) == b) {
             if (!waited) { q->submit_waits.fetch_add(1, std::memory_order_relaxed); waited = true; }
             q->cv_open.wait(lk, [&] { return q->open.load(std::memory_order_acquire) != b; });
-            note_max(q->max_submit_wait, now_ns() - t_w);
+            const int64_t t_ww = now_ns();
+            note_max(q->max_submit_wait, t_ww - t_w);
+            static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+            if (trace && t_ww - t_w > 1000000)
+                fprintf(stderr, "lcb_hash_queue: t=%.0f us a submit waited %.0f us for an open slot\n",
+                        (t_w - q->t_create) * 1e-3, (t_ww - t_w) * 1e-3);
         }
     }
 }
