@@ -1118,22 +1118,24 @@ def main():
                         r["fixed_stride_ratio_per_block_equal_clock"] = round(
                             r["fixed_stride_ratio_per_block"] * per[name]["clock"]["clock_GHz"] /
                             r["clock"]["clock_GHz"], 3)
-        # HMAC-MD5 on C4 (segmented long waves through the
-        # HMAC tile kernel's one copy), its per-compression ratio to the
-        # fixed-stride HMAC-MD5 row above (HMAC: one outer compression more
-        # per message).
-        c4h = bench_c4([ALG_IDS["md5"]], 1, 3, key=key)["hmac_md5"]
+        # HMAC on C4 (segmented long waves through the
+        # HMAC tile kernel's one copy; MD5, SHA-1, SHA-256), each with its
+        # per-compression ratio to the fixed-stride HMAC row above (HMAC: one
+        # outer compression more per message).
+        c4hs = bench_c4([ALG_IDS[n] for n in ("md5", "sha1", "sha256")], 1, 3, key=key)
 
         def hmac_blocks_per_byte(lens):
             return float((((lens + 1 + 8 + 63) // 64) + 1).sum() * 64) / float(lens.sum())
-        c4h["fixed_stride_GiB_s"] = hm["hmac_md5"]["GiB_s"]
-        c4h["fixed_stride_ratio_per_block"] = round(
-            c4h["GiB_s"] / hm["hmac_md5"]["GiB_s"] * hmac_blocks_per_byte(c4_lens) /
-            hmac_blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
-        if c4h.get("clock") and hm["hmac_md5"].get("clock_GHz"):
-            c4h["fixed_stride_ratio_per_block_equal_clock"] = round(
-                c4h["fixed_stride_ratio_per_block"] * hm["hmac_md5"]["clock_GHz"] / c4h["clock"]["clock_GHz"], 3)
-        c4["hmac_md5"] = c4h
+        for hname, c4h in c4hs.items():
+            fx = hm[hname]
+            c4h["fixed_stride_GiB_s"] = fx["GiB_s"]
+            c4h["fixed_stride_ratio_per_block"] = round(
+                c4h["GiB_s"] / fx["GiB_s"] * hmac_blocks_per_byte(c4_lens) /
+                hmac_blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+            if c4h.get("clock") and fx.get("clock_GHz"):
+                c4h["fixed_stride_ratio_per_block_equal_clock"] = round(
+                    c4h["fixed_stride_ratio_per_block"] * fx["clock_GHz"] / c4h["clock"]["clock_GHz"], 3)
+            c4[hname] = c4h
         out["ragged_c4_per_alg"] = c4
         out["ragged_packets"] = bench_packets(10, max(3, a.steps // 4),
                                               ref_clock=clock["clock_GHz"] if clock else None)

@@ -766,19 +766,19 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
     const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
     const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
-    // Segmented jobs: plain digests of MD5, SHA-1 and SHA-256 only
-    // (launch_ordered).  Each segmented copy of the line loop adds about as
+    // Segmented jobs: plain and HMAC digests of MD5, SHA-1 and SHA-256
+    // only (launch_ordered).  Each segmented copy of the line loop adds about as
     // much machine code as the unsegmented one, and the code object's size
     // showed in the headline: a library with segmented copies for every
     // mode (33 MB) ran its first 20 timed fixed-stride steps 7 % slower than
     // one without (18 MB), the same kernel, fresh processes alternating
     // (profiles/r6_codesize_headline.txt).
-    // HMAC-MD5 takes segmented jobs through ONE copy
-    // of its line loop, the segmented one, for segmented and whole tiles
-    // alike: no second copy, so no code growth (the packet tiles pay the
-    // segment paths' registers: one copy with both paths ran the plain
-    // packets 0.5 % slower, below).
-    constexpr bool kSegHmac = kMode == kTileHmac && std::is_same<H, Md5>::value;
+    // HMAC (MD5, SHA-1, SHA-256) takes segmented jobs
+    // through ONE copy of its line loop, the segmented one, for segmented
+    // and whole tiles alike: no second copy, so no code growth (the packet
+    // tiles pay the segment paths' registers: one copy with both paths ran
+    // the plain packets 0.5 % slower, below).
+    constexpr bool kSegHmac = kMode == kTileHmac && !std::is_same<H, Sha256<true>>::value;
     constexpr bool kSegMode = (kMode == kTilePlain && !std::is_same<H, Sha256<true>>::value) || kSegHmac;
     const bool uniform = __all(Rl == R);
     if (js.nsegs > 1 && (!kSegMode || !uniform)) {
