@@ -476,7 +476,7 @@ int hmac_setup(int alg, const uint8_t* key, size_t key_len, hipStream_t s, const
 static uint32_t seg_capacity(int alg, const KArgs& a) {
     if (!a.lengths || a.order != nullptr || a.count < kBucketMinCount || a.count >= kBucketMaxCount) return 0;
     const bool tiles = tiles_take(alg, a);
-    const bool seg_kernel = tiles ? a.key_mode == kKeyNone && (alg == 1 || alg == 2 || alg == 4)
+    const bool seg_kernel = tiles ? a.key_mode == kKeyNone && alg >= 1 && alg <= 4
                                   : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
     if (!seg_kernel) return 0;
     const char* ev = getenv("LCB_TILE_SEGS");

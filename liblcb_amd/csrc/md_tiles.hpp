@@ -766,20 +766,22 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
     // The tile's dword phase R (uniform after the bucketing), or a mixed tile.
     const uint32_t Rl = ((uint32_t)reinterpret_cast<uintptr_t>(r.p) >> 2) & 3u;
     const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane(Rl);
-    // Segmented jobs: plain and HMAC digests of MD5, SHA-1 and SHA-256
-    // only (launch_ordered).  Each segmented copy of the line loop adds about as
-    // much machine code as the unsegmented one, and the code object's size
-    // showed in the headline: a library with segmented copies for every
-    // mode (33 MB) ran its first 20 timed fixed-stride steps 7 % slower than
-    // one without (18 MB), the same kernel, fresh processes alternating
-    // (profiles/r6_codesize_headline.txt).
-    // HMAC (MD5, SHA-1, SHA-256) takes segmented jobs
-    // through ONE copy of its line loop, the segmented one, for segmented
-    // and whole tiles alike: no second copy, so no code growth (the packet
+    // Segmented jobs: plain and HMAC digests of MD5, SHA-1 and SHA-224/256
+    // (launch_ordered; not the keyed modes).  Each segmented copy of the
+    // line loop adds about as much machine code as the unsegmented one, and
+    // the code object's size showed in the headline: a library with
+    // segmented copies for every mode (33 MB) ran its first 20 timed
+    // fixed-stride steps 7 % slower than one without (18 MB), the same
+    // kernel, fresh processes alternating (profiles/r6_codesize_headline.txt).
+    // HMAC and plain SHA-224 take segmented jobs through
+    // ONE copy of their line loop, the segmented one, for segmented and
+    // whole tiles alike: no second copy, so no code growth (their packet
     // tiles pay the segment paths' registers: one copy with both paths ran
-    // the plain packets 0.5 % slower, below).
-    constexpr bool kSegHmac = kMode == kTileHmac && !std::is_same<H, Sha256<true>>::value;
-    constexpr bool kSegMode = (kMode == kTilePlain && !std::is_same<H, Sha256<true>>::value) || kSegHmac;
+    // the plain MD5 packets 0.5 % slower).  Plain MD5, SHA-1 and SHA-256
+    // keep two copies (the packet rows run the unsegmented one).
+    constexpr bool kSha224 = std::is_same<H, Sha256<true>>::value;
+    constexpr bool kOneCopy = kMode == kTileHmac || (kMode == kTilePlain && kSha224);
+    constexpr bool kSegMode = kMode == kTilePlain || kOneCopy;
     const bool uniform = __all(Rl == R);
     if (js.nsegs > 1 && (!kSegMode || !uniform)) {
         // a segmented tile that cannot be cut: segment 0 runs it whole (one
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(64, H::kTileOcc) void md_tiles_kernel(KArgs a) {
         js.nsegs = 1;
     }
     if (uniform) {
-        if constexpr (kSegMode && (LCB_TILE_ONECOPY || kSegHmac)) {
+        if constexpr (kSegMode && (LCB_TILE_ONECOPY || kOneCopy)) {
             md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));
         } else if constexpr (kSegMode) {
             if (js.nsegs > 1) md_tile_phase<H, kMode, true>(a, r, lane, slab, js, R LCB_TRACE(, tr));

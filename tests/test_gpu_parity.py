@@ -583,7 +583,7 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("alg,key", [(1, None), (1, b"seg-hmac-key"), (2, None), (2, b"seg-hmac-key" * 7),
-                                     (4, None), (4, b"k"), (6, None)])
+                                     (3, None), (3, b"224"), (4, None), (4, b"k"), (6, None)])
 def test_segmented_takeover(gpu, alg, key, monkeypatch):
     """the take-over path of segmented jobs (seg_jobs.hpp
     seg_wait): with LCB_SEG_TAKEOVER=1 the jobs of every cut wave run in
