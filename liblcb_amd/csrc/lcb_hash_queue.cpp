@@ -24,6 +24,10 @@
 // datagram to a callback that hashes it (include/proto/radius.h:776-830);
 // completion mirrors tpt_msg_send() (src/threadpool/threadpool_msg_sys.c:279).
 #include <errno.h>
+#include <execinfo.h>
+#include <unistd.h>
+#include <pthread.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -213,6 +217,13 @@ struct lcb_hash_queue_s {
     std::atomic<int> nregions{0};
 
     std::thread flusher, completer;
+    // LCB_QUEUE_TRACE=2: a watchdog samples the flusher's stack while one
+    // launch's enqueues take over 2 ms (what a blocking enqueue waits in).
+    std::thread watchdog;
+    std::atomic<int64_t> enq_t0{0};          // flusher: start of the current launch's enqueues, 0 outside
+    std::atomic<bool> watchdog_stop{false};
+    pthread_t flusher_tid{};
+    void watchdog_main();
 
     void flusher_main();
     void completer_main();
@@ -368,6 +379,7 @@ void lcb_hash_queue_s::launch(Slot* b, int why, int64_t* steps) {
     a.count = b->n; a.stride = 0; a.fixed_len = 0; a.digests = b->h_dig; a.mid = mid;
     int rc = 0;
     tt[1] = now_ns();
+    enq_t0.store(tt[1], std::memory_order_release);
     if (hipMemcpyAsync(b->d_off, b->h_off, b->n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b->d_len, b->h_len, b->n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
         (aused && hipMemcpyAsync(b->d_data, b->h_data, aused, hipMemcpyHostToDevice, st) != hipSuccess))
@@ -382,6 +394,7 @@ void lcb_hash_queue_s::launch(Slot* b, int why, int64_t* steps) {
     tt[4] = now_ns();
     if (!rc && hipEventRecord(b->done, st) != hipSuccess) rc = EIO;
     tt[5] = now_ns();
+    enq_t0.store(0, std::memory_order_release);
     for (int k = 0; k < 5; ++k) steps[k] = tt[k + 1] - tt[k];
     // LCB_QUEUE_TRACE=1: report any launch over 1 ms on stderr as well.
     static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
@@ -492,6 +505,37 @@ void lcb_hash_queue_s::flusher_main() {
             if (trace && now_ns() - t_fw > 1000000)
                 fprintf(stderr, "lcb_hash_queue: t=%.0f us flusher waited %.0f us for a free slot (%zu in flight)\n",
                         (t_fw - t_create) * 1e-3, (now_ns() - t_fw) * 1e-3, nin);
+        }
+    }
+}
+
+namespace {
+void stack_sample_handler(int) {
+    void* fr[48];
+    const int n = backtrace(fr, 48);
+    static const char hdr[] = "lcb_hash_queue: flusher stack while an enqueue blocks:\n";
+    (void)!write(2, hdr, sizeof hdr - 1);
+    backtrace_symbols_fd(fr, n, 2);
+}
+}  // namespace
+
+void lcb_hash_queue_s::watchdog_main() {
+    void* warm[4];
+    (void)backtrace(warm, 4);   // load the unwinder outside the signal handler
+    int64_t sampled_t0 = 0;
+    int samples = 0;
+    while (!watchdog_stop.load(std::memory_order_acquire)) {
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+        const int64_t t0 = enq_t0.load(std::memory_order_acquire);
+        if (t0 == 0) continue;
+        if (t0 != sampled_t0) { sampled_t0 = t0; samples = 0; }
+        const int64_t age = now_ns() - t0;
+        // up to 3 samples per blocked launch, 2 ms apart, from 2 ms on
+        if (samples < 3 && age > 2000000ll * (samples + 1)) {
+            fprintf(stderr, "lcb_hash_queue: t=%.0f us launch enqueues blocked %.0f us, sampling the flusher\n",
+                    (t0 - t_create) * 1e-3, age * 1e-3);
+            pthread_kill(flusher_tid, SIGUSR2);
+            ++samples;
         }
     }
 }
@@ -734,6 +778,18 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
     }
     q->flusher = std::thread([q] { q->flusher_main(); });
     q->completer = std::thread([q] { q->completer_main(); });
+    {
+        const char* tr = getenv("LCB_QUEUE_TRACE");
+        if (tr && atoi(tr) >= 2) {
+            struct sigaction sa {};
+            sa.sa_handler = stack_sample_handler;
+            sigemptyset(&sa.sa_mask);
+            sa.sa_flags = SA_RESTART;
+            sigaction(SIGUSR2, &sa, nullptr);
+            q->flusher_tid = q->flusher.native_handle();
+            q->watchdog = std::thread([q] { q->watchdog_main(); });
+        }
+    }
     *q_out = q;
     return 0;
 }
@@ -959,6 +1015,8 @@ void lcb_hash_queue_destroy(lcb_hash_queue_p q) {
         q->stop = true;
     }
     q->cv_flusher.notify_all();
+    q->watchdog_stop.store(true, std::memory_order_release);
+    if (q->watchdog.joinable()) q->watchdog.join();
     q->flusher.join();
     {
         std::lock_guard<std::mutex> lk(q->m);
