@@ -1016,7 +1016,10 @@ def main():
                      # engine clock of the timed launches (rank 0's), and the
                      # VALU floor at that clock
                      "clock": clock,
-                     "valu_frac_run_clock_4c": valu_frac_at(vfloor, clock, kms),
+                     # the same with a flat 4 cycles per VALU instruction:
+                     # a model check, not a fraction (above 1 where the mix
+                     # issues faster, hence valu_cpi)
+                     "valu_4cycle_model_ratio": valu_frac_at(vfloor, clock, kms),
                      "valu_cpi": valu_cpi(alg),
                      "valu_frac_run_clock": valu_frac_at(vfloor, clock, kms, valu_cpi(alg))},
     }
@@ -1063,7 +1066,7 @@ def main():
                          "hbm_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "valu_frac": round(vf / km, 4) if vf else None,
                          "clock": ck, "valu_cpi": valu_cpi(aid),
-                         "valu_frac_run_clock_4c": valu_frac_at(vf, ck, km),
+                         "valu_4cycle_model_ratio": valu_frac_at(vf, ck, km),
                          "valu_frac_run_clock": valu_frac_at(vf, ck, km, valu_cpi(aid))}
             if name.startswith("gost"):
                 # GOST is bound by its LDS table gathers, not HBM or VALU:
