@@ -1109,18 +1109,23 @@ def main():
             if name in per:
                 r["fixed_stride_GiB_s"] = per[name]["GiB_s"]
                 blk = {"sha384": (128, 16), "sha512": (128, 16)}.get(name, (64, 8))
-                if not name.startswith("gost"):
-                    def blocks_per_byte(lens):
-                        return float(((lens + 1 + blk[1] + blk[0] - 1) // blk[0]).sum() * blk[0]) / float(lens.sum())
-                    r["fixed_stride_ratio_per_block"] = round(
-                        r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
-                        blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
-                    # the same at equal engine clocks (both passes' in-run
-                    # clocks: VALU-bound kernels scale with it)
-                    if r.get("clock") and per[name].get("clock"):
-                        r["fixed_stride_ratio_per_block_equal_clock"] = round(
-                            r["fixed_stride_ratio_per_block"] * per[name]["clock"]["clock_GHz"] /
-                            r["clock"]["clock_GHz"], 3)
+
+                def blocks_per_byte(lens):
+                    if name.startswith("gost"):
+                        # Streebog: floor(len / 64) full blocks + 1 padded
+                        # block, then the N and Sigma finalisation
+                        # compressions (gost3411-2012.h)
+                        return float(((lens // 64) + 3).sum() * 64) / float(lens.sum())
+                    return float(((lens + 1 + blk[1] + blk[0] - 1) // blk[0]).sum() * blk[0]) / float(lens.sum())
+                r["fixed_stride_ratio_per_block"] = round(
+                    r["GiB_s"] / per[name]["GiB_s"] * blocks_per_byte(c4_lens) /
+                    blocks_per_byte(np.array([MSG_LEN], np.uint64)), 3)
+                # the same at equal engine clocks (both passes' in-run
+                # clocks: VALU-bound kernels scale with it)
+                if r.get("clock") and per[name].get("clock"):
+                    r["fixed_stride_ratio_per_block_equal_clock"] = round(
+                        r["fixed_stride_ratio_per_block"] * per[name]["clock"]["clock_GHz"] /
+                        r["clock"]["clock_GHz"], 3)
         # HMAC on C4 (segmented long waves through the
         # HMAC tile kernel's one copy; MD5, SHA-1, SHA-256), each with its
         # per-compression ratio to the fixed-stride HMAC row above (HMAC: one
