@@ -774,20 +774,30 @@ def bench_crc(data, count, steps):
     out_t = torch.empty(count, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
     res = {}
-    for v, name in CRC_NAMES.items():
-        def launch():
-            check(lib().lcb_crc32_batch(v, None, data.data_ptr(), None, None, count, MSG_LEN, MSG_LEN,
-                                        out_t.data_ptr(), F_DEVICE, stream.cuda_stream))
-        for _ in range(10):
-            launch()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
-        for e0, e1 in ev:
-            e0.record(stream)
-            launch()
-            e1.record(stream)
+
+    def crc_launch(v):
+        check(lib().lcb_crc32_batch(v, None, data.data_ptr(), None, None, count, MSG_LEN, MSG_LEN,
+                                    out_t.data_ptr(), F_DEVICE, stream.cuda_stream))
+    # HBM-bound after VALU-bound rows: the memory side's clocks ramp back
+    # over tens of ms (the variants timed in a row ran 0.51 -> 0.69 of HBM
+    # with 10 warm launches each, r8d), so the family is warmed for 150 ms
+    # first; then each variant: 10 warm launches and `steps` timed between
+    # two events.
+    t_end = time.time() + 0.15
+    while time.time() < t_end:
+        for _ in range(20):
+            crc_launch(next(iter(CRC_NAMES)))
         torch.cuda.synchronize()
-        km = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+    for v, name in CRC_NAMES.items():
+        for _ in range(10):
+            crc_launch(v)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            crc_launch(v)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        km = e0.elapsed_time(e1) / steps
         res[name] = {"GiB_s": round(count * MSG_LEN / (km * 1e-3) / 2**30, 2), "kernel_ms": round(km, 4),
                      "hbm_frac": round(count * (MSG_LEN + 4) / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     del out_t

@@ -560,6 +560,58 @@ __device__ __forceinline__ void gost_sigma_add(uint64_t sg[8], const uint32_t w[
 // kernel is LDS-bound at ~0.04 of HBM) right before the last g_0(h, Sigma)
 // (:1837).  Sigma costs no VGPRs and no LDS through the 19 g's of a 1 KiB
 // message, and nothing is live across g_0(h, N) but h.
+// The two-pass form in two parts, for segmented long waves (gost_seg_kernel):
+// the chain over whole blocks [j0, j1) ...
+template <class G, class Src, class Tab>
+__device__ __forceinline__ void gost_chain_blocks(G& st, const Src& src, const Tab& T, uint64_t j0, uint64_t j1) {
+    uint32_t w[16];
+    for (uint64_t j = j0; j < j1; ++j) {
+#if LCB_LANE_PRIO
+        if ((j & 15) == 0) wave_prio_left((j1 - j) * 64u);
+#endif
+        src.block(j, w);
+        st.chain(w, 512, T);
+    }
+}
+// ... and the rest after the last whole block: the tail || 0x01 block,
+// g_0(h, N), the Sigma pass over the whole message, g_0(h, Sigma).
+template <class G, class Src, class Tab>
+__device__ __forceinline__ void gost_run2_final(G& st, const Src& src, const Tab& T) {
+    uint32_t w[16];
+    const uint64_t nfull = src.nfull();
+    const uint32_t rem = src.rem();
+    src.tail_n(w, rem);
+    put_byte(w, rem, 0x01u);
+    st.chain(w, (uint64_t)rem * 8u, T);
+    {
+        uint64_t m[8], ml[8];
+        m[0] = st.get_n();
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m[i] = 0;
+        T.to_lane(ml, m);
+        gost_g(st.h, 0, ml, T);                   // g_0(h, N)
+    }
+    uint64_t sg[8], sl[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sg[i] = 0;
+    const Src s2 = src.opaque();
+    for (uint64_t j = 0; j < nfull; ++j) {
+        s2.block(j, w);
+        gost_sigma_add(sg, w);
+    }
+    // The tail's byte masks re-formed from an opaque copy of rem: else they
+    // are computed once and kept (spilled) across the chain.
+    uint32_t r2 = rem;
+    asm volatile("" : "+v"(r2));
+    s2.tail_n(w, r2);
+    put_byte(w, r2, 0x01u);
+    gost_sigma_add(sg, w);
+    T.to_lane(sl, sg);
+    gost_g(st.h, 0, sl, T);                       // g_0(h, Sigma)
+}
+// gost_run2 = gost_chain_blocks(0, nfull) + gost_run2_final, written out
+// as one body: that is the machine code the plain kernel was tuned on (the
+// split form compiles to different code at the same 124 VGPRs).
 template <class G, class Src, class Tab>
 __device__ __forceinline__ void gost_run2(G& st, const Src& src, const Tab& T) {
     uint32_t w[16];
@@ -591,8 +643,6 @@ __device__ __forceinline__ void gost_run2(G& st, const Src& src, const Tab& T) {
         s2.block(j, w);
         gost_sigma_add(sg, w);
     }
-    // The tail's byte masks re-formed from an opaque copy of rem: else they
-    // are computed once and kept (spilled) across the chain.
     uint32_t r2 = rem;
     asm volatile("" : "+v"(r2));
     s2.tail_n(w, r2);

@@ -4,6 +4,7 @@
 #include "gost_device.hpp"
 #include "hash_device.hpp"
 #include "lcb_internal.hpp"
+#include "seg_jobs.hpp"
 
 namespace lcbgpu {
 
@@ -123,6 +124,66 @@ __global__ __launch_bounds__(kGostPlainThreads, 4) void gost_plain2_kernel(KArgs
     st.digest_words(dw, T);
     settle_words<G::kDigest / 4>(dw);
     store_digest<G::kDigest>(a.digests + store_index(a, base) * G::kDigest, dw);
+}
+
+// Plain GOST batches with segmented long waves (a.seg: the bucketing cut
+// the longest class's waves into kSegs jobs, seg_jobs.hpp).  C4 (a third of
+// 1M records 64 KiB long) ran 0.89 of the fixed-stride rate per compression
+// unsegmented: 5,468 waves of 64 KiB records over 4,096 wave slots end in a
+// partly filled second generation.  Job j of the grid is wave-level (8 per
+// workgroup); a segment chains its lanes' whole blocks [n s / S, n (s + 1)
+// / S) -- per lane, n = that lane's whole blocks -- and hands h (16 words)
+// on; N = 512 x the blocks before it, so only h travels.  The last segment
+// also runs the tail, g_0(h, N) and the Sigma pass over the whole message
+// (gost_run2_final).  The same occupancy as gost_plain2_kernel; a separate
+// kernel so that the plain one keeps its machine code.
+template <bool k256>
+__global__ __launch_bounds__(kGostPlainThreads, 4) void gost_seg_kernel(KArgs a) {
+    __shared__ __attribute__((aligned(256))) uint64_t Timg[256 * 32];  // 64 KiB rotated image
+    gost_stage_rot(Timg);
+    GostRotF<0> T;
+    T.init((lds_u8*)Timg);
+    TileSeg js;
+    const uint64_t wv = seg_job(a, (uint64_t)blockIdx.x * (kGostPlainThreads / 64) + (threadIdx.x >> 6), js);
+    if (wv * 64 >= a.count) return;   // wave-uniform: the grid is an upper bound
+    const uint64_t i = wv * 64 + (threadIdx.x & 63);
+    const bool valid = i < a.count;
+    uint64_t idx = 0, len = 0;
+    const uint8_t* msg = gptr(a.data);
+    if (valid) msg_at(a, i, idx, msg, len);
+    using G = Gost<k256>;
+    G st;
+    st.init();
+    const GostPlainSrc src{msg, len};
+    const uint64_t nfull = src.nfull();
+    uint64_t j0 = 0, j1 = nfull;
+    bool last = true;
+    if (js.nsegs > 1) {
+        bool whole = false;
+        if (js.seg > 0) {
+            if (!seg_wait(js, &whole)) return;   // taken over by another job
+            if (!whole) {
+                j0 = nfull * js.seg / js.nsegs;
+                seg_load(st.h, js.lane_state());
+                st.set_n(512 * j0);
+            }
+        }
+        if (!whole && js.seg + 1 < js.nsegs) {
+            j1 = nfull * (js.seg + 1) / js.nsegs;
+            last = false;
+        }
+    }
+    gost_chain_blocks(st, src, T, j0, j1);
+    if (!last) {
+        seg_save(st.h, js.lane_state());
+        seg_publish(js.flag, js.seg);
+        return;
+    }
+    gost_run2_final(st, src, T);
+    uint32_t dw[G::kDigest / 4];
+    st.digest_words(dw, T);
+    settle_words<G::kDigest / 4>(dw);
+    if (valid) store_digest<G::kDigest>(a.digests + idx * G::kDigest, dw);
 }
 
 // Diagnostic (lcb_hash_gpu_read_probe LCB_PROBE_GOST_LPS): the bound of the
@@ -300,6 +361,11 @@ void launch_gost(const KArgs& a, bool hmac, hipStream_t s) {
     if (hmac) {
         auto k = gost_hmac_kernel<k256>;
         hipLaunchKernelGGL(k, gost_grid(k, a.count), dim3(kGostThreads), 0, s, a);
+    } else if (a.seg) {
+        // waves + (kSegs - 1) x the segment capacity: an upper bound of the jobs
+        const uint64_t jobs = (a.count + 63) / 64 + (uint64_t)(kSegs - 1) * a.seg_cap;
+        const dim3 g((unsigned)((jobs + kGostPlainThreads / 64 - 1) / (kGostPlainThreads / 64)));
+        hipLaunchKernelGGL(gost_seg_kernel<k256>, g, dim3(kGostPlainThreads), 0, s, a);
     } else {
         const dim3 g((unsigned)((a.count + kGostPlainThreads - 1) / kGostPlainThreads));
         hipLaunchKernelGGL(gost_plain2_kernel<k256>, g, dim3(kGostPlainThreads), 0, s, a);

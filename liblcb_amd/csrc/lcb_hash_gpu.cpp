@@ -477,7 +477,8 @@ static uint32_t seg_capacity(int alg, const KArgs& a) {
     if (!a.lengths || a.order != nullptr || a.count < kBucketMinCount || a.count >= kBucketMaxCount) return 0;
     const bool tiles = tiles_take(alg, a);
     const bool seg_kernel = tiles ? a.key_mode == kKeyNone && alg >= 1 && alg <= 4
-                                  : (alg == 5 || alg == 6) && a.key_mode == kKeyNone;
+                                  : a.key_mode == kKeyNone && (alg == 5 || alg == 6 ||
+                                                               ((alg == 7 || alg == 8) && a.mid == nullptr));
     if (!seg_kernel) return 0;
     const char* ev = getenv("LCB_TILE_SEGS");
     if (ev && ev[0] == '0') return 0;

@@ -753,7 +753,7 @@ void launch_bucketing(const KArgs& a, uint32_t* work, uint32_t* order, bool tile
 
 uint32_t tile_slots(int alg) {
     // 4 SIMDs per CU x the batch kernel's waves per SIMD: the tile kernel's,
-    // or md_lines_kernel's for SHA-384/512.
+    // md_lines_kernel's for SHA-384/512, the plain GOST kernels'.
     uint32_t occ = 0;
     switch (alg) {
     case 1: occ = Md5::kTileOcc; break;
@@ -762,6 +762,8 @@ uint32_t tile_slots(int alg) {
     case 4: occ = Sha256<false>::kTileOcc; break;
     case 5:
     case 6: occ = kLinesOcc; break;
+    case 7:
+    case 8: occ = 4; break;   // gost_plain2_kernel / gost_seg_kernel: 2 x 512-thread workgroups per CU
     default: break;
     }
     return occ * 4u * (uint32_t)device_cu_count();

@@ -583,7 +583,8 @@ def test_segmented_long_tiles(gpu, oracle, alg, key, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("alg,key", [(1, None), (1, b"seg-hmac-key"), (2, None), (2, b"seg-hmac-key" * 7),
-                                     (3, None), (3, b"224"), (4, None), (4, b"k"), (6, None)])
+                                     (3, None), (3, b"224"), (4, None), (4, b"k"), (6, None), (7, None),
+                                     (8, None)])
 def test_segmented_takeover(gpu, alg, key, monkeypatch):
     """the take-over path of segmented jobs (seg_jobs.hpp
     seg_wait): with LCB_SEG_TAKEOVER=1 the jobs of every cut wave run in
@@ -595,7 +596,8 @@ def test_segmented_takeover(gpu, alg, key, monkeypatch):
     (lcb_hash_gpu_seg_last) show the waves taken over."""
     import ctypes
     # lengths within 7/8 of each other (61,440..65,536 B), so a tile's
-    # whole-block lines are most of it and it is cut (md_tiles.hpp)
+    # whole-block lines are most of it and it is cut (md_tiles.hpp); GOST:
+    # gost_seg_kernel, 4 waves per SIMD like MD5's tiles
     tiles = 2726 if alg in (2, 3, 4) else 5456
     n = tiles * 64
     rng = np.random.default_rng(160 + alg)
@@ -626,7 +628,7 @@ def test_segmented_takeover(gpu, alg, key, monkeypatch):
     # and the normal order again (the knob is per call)
     again = gpu.hash_batch(alg, data, offsets=do, lengths=dl, key=key).cpu().numpy()
     assert np.array_equal(again, whole), alg
-    if key is not None:   # HMAC-MD5's segmented tiles against the oracle, sampled
+    if key is not None or alg in (7, 8):   # HMAC tiles and GOST segments against the oracle, sampled
         from oracle.pyoracle import Oracle
         pick = np.sort(rng.choice(n, 64, replace=False))
         parts, soff, pos = [], np.zeros(len(pick), np.uint64), 0
