@@ -147,6 +147,13 @@ int	lcb_hash_queue_flush(lcb_hash_queue_p q);
 int	lcb_hash_queue_wait(lcb_hash_queue_p q);
 int	lcb_hash_queue_stats(lcb_hash_queue_p q, lcb_hash_queue_stats_t *st);
 
+/* Diagnostics (environment, read once per process): LCB_QUEUE_TRACE=1 logs
+ * every stall over 1 ms to stderr (a slow launch step, a batch the
+ * completion thread picked up late, the flusher waiting for a free slot, a
+ * submit waiting for an open slot, a batch slower than 1 ms end to end);
+ * LCB_QUEUE_TRACE=2 also samples the flusher's stack (it takes SIGUSR2 for
+ * the process) while one launch's enqueues take over 2 ms. */
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,19 @@ constexpr uint64_t kZeroCopyTag = 1ull << 63;
 // between two packets of one run (bytes copied but never hashed).
 constexpr int kZcRuns = 32;
 constexpr uint64_t kZcGap = 256;
+// LCB_QUEUE_TRACE (read once): 1 logs every stall over 1 ms on stderr (a
+// slow launch step, a batch picked up late by the completion thread, the
+// flusher waiting for a free slot, a submit waiting for an open slot, a
+// batch slower than 1 ms end to end); 2 also starts a watchdog that samples
+// the flusher's stack (SIGUSR2, taken for the whole process) while one
+// launch's enqueues take over 2 ms.  Diagnostics only.
+int trace_level() {
+    static const int lv = [] {
+        const char* e = getenv("LCB_QUEUE_TRACE");
+        return e ? atoi(e) : 0;
+    }();
+    return lv;
+}
 inline uint64_t st_bytes(uint64_t s) { return s & kBytesMask; }
 
 struct Meta {
@@ -397,7 +410,7 @@ void lcb_hash_queue_s::launch(Slot* b, int why, int64_t* steps) {
     enq_t0.store(0, std::memory_order_release);
     for (int k = 0; k < 5; ++k) steps[k] = tt[k + 1] - tt[k];
     // LCB_QUEUE_TRACE=1: report any launch over 1 ms on stderr as well.
-    static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+    const bool trace = trace_level() > 0;
     if (trace && tt[5] - tt[0] > 1000000)
         fprintf(stderr, "lcb_hash_queue: slow launch seq=%llu n=%zu runs=%d aused=%llu: rebase %.0f us, "
                 "idx/len %.0f us, runs %.0f us, kernel %.0f us, event %.0f us\n", (unsigned long long)b->seq, b->n,
@@ -475,7 +488,7 @@ void lcb_hash_queue_s::flusher_main() {
         const int64_t t_busy = now_ns();
         drain_leases(b);
         const int64_t t_launch = now_ns();
-        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+        const bool trace = trace_level() > 0;
         if (trace && (t_launch - t_busy > 1000000 || t_busy - b->t_seal > 1000000))
             fprintf(stderr, "lcb_hash_queue: slow seal -> launch: reopen %.0f us, drain %.0f us\n",
                     (t_busy - b->t_seal) * 1e-3, (t_launch - t_busy) * 1e-3);
@@ -552,7 +565,7 @@ void lcb_hash_queue_s::completer_main() {
             b = inflight.front();
         }
         const int64_t t_wait = now_ns();
-        static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+        const bool trace = trace_level() > 0;
         if (trace && t_wait - std::max(prev_end, b->t_launch) > 1000000)
             fprintf(stderr, "lcb_hash_queue: t=%.0f us completer took batch seq=%llu up %.0f us late\n",
                     (t_wait - t_create) * 1e-3, (unsigned long long)b->seq,
@@ -779,8 +792,7 @@ int lcb_hash_queue_create(int alg, const uint8_t* key, size_t key_len, const lcb
     q->flusher = std::thread([q] { q->flusher_main(); });
     q->completer = std::thread([q] { q->completer_main(); });
     {
-        const char* tr = getenv("LCB_QUEUE_TRACE");
-        if (tr && atoi(tr) >= 2) {
+        if (trace_level() >= 2) {
             struct sigaction sa {};
             sa.sa_handler = stack_sample_handler;
             sigemptyset(&sa.sa_mask);
@@ -920,7 +932,7 @@ int lcb_hash_queue_submitv(lcb_hash_queue_p q, const lcb_hash_seg_t* segs, size_
             q->cv_open.wait(lk, [&] { return q->open.load(std::memory_order_acquire) != b; });
             const int64_t t_ww = now_ns();
             note_max(q->max_submit_wait, t_ww - t_w);
-            static const bool trace = getenv("LCB_QUEUE_TRACE") && atoi(getenv("LCB_QUEUE_TRACE")) > 0;
+            const bool trace = trace_level() > 0;
             if (trace && t_ww - t_w > 1000000)
                 fprintf(stderr, "lcb_hash_queue: t=%.0f us a submit waited %.0f us for an open slot\n",
                         (t_w - q->t_create) * 1e-3, (t_ww - t_w) * 1e-3);
