@@ -644,6 +644,45 @@ def test_segmented_takeover(gpu, alg, key, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alg", [7, 8])
+def test_gost_segmented_mixed_lengths(gpu, alg, monkeypatch):
+    """Plain GOST's segmented long waves (gost_seg_kernel) in the normal
+    order, on lengths that vary inside a wave: 300K records of 32..160 KiB
+    at random lengths (not multiples of 64; two to three length classes, so
+    a cut wave's lanes hold different block counts and each lane cuts its own
+    chain in thirds) after 60K short records (the bucketing puts the long
+    class first either way).  Digests equal the same batch unsegmented
+    (LCB_TILE_SEGS=0) and a sample equals the oracle."""
+    from oracle.pyoracle import Oracle
+    rng = np.random.default_rng(700 + alg)
+    n_long, n_short = 5200 * 64, 60000
+    lens = np.concatenate([rng.integers(0, 2000, n_short), rng.integers(32768, 163841, n_long)]).astype(np.uint32)
+    rng.shuffle(lens)
+    offs = np.zeros(len(lens), np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 8, len(lens) - 1).astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 64
+    data = gpu.gen_synthetic(0x6057 + alg, total)
+    do = torch.as_tensor(offs.astype(np.int64), device="cuda")
+    dl = torch.as_tensor(lens.astype(np.int32), device="cuda")
+    seg = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    monkeypatch.setenv("LCB_TILE_SEGS", "0")
+    whole = gpu.hash_batch(alg, data, offsets=do, lengths=dl).cpu().numpy()
+    monkeypatch.delenv("LCB_TILE_SEGS")
+    assert np.array_equal(seg, whole), alg
+    pick = np.sort(rng.choice(len(lens), 48, replace=False))
+    parts, soff, pos = [], np.zeros(len(pick), np.uint64), 0
+    for j, i in enumerate(pick):
+        o, ln = int(offs[i]), int(lens[i])
+        parts.append(data[o:o + ln].cpu().numpy())
+        soff[j] = pos
+        pos += ln
+    exp = Oracle().batch(alg, np.concatenate(parts), soff, lens[pick])
+    assert np.array_equal(seg[pick], exp), alg
+    del data
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("alg", [1, 6])
 def test_bucketing_one_kernel_form(gpu, alg, monkeypatch):
     """The one-kernel bucketing (LCB_BUCKET_FUSED=1, lcb_kernels.hip
