@@ -887,7 +887,7 @@ def bench_ingest(alg_id, packets=1 << 21, threads=8):
         if r.returncode != 0:
             raise RuntimeError(r.stderr.strip()[-300:])
         out = json.loads(r.stdout.strip().splitlines()[-1])
-        out["stall_trace"] = [ln.strip() for ln in r.stderr.splitlines() if "lcb_hash_queue:" in ln][:8]
+        out["stall_trace"] = [ln.strip() for ln in r.stderr.splitlines() if "lcb_hash_queue:" in ln][:12]
         out["cgroup_throttled"] = None if t0 is None or t1 is None else \
             {"periods": t1[0] - t0[0], "us": round(t1[1] - t0[1], 1)}
         return out
